@@ -1,0 +1,59 @@
+// Shared device/host definitions for libspk_hip (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstddef>
+#include <string>
+
+namespace spk {
+
+// Fused epilogue activations (applied after bias + residual).
+enum Act : int {
+  ACT_NONE = 0,
+  ACT_RELU = 1,      // max(x, 0)                       (F.relu / nn.ReLU)
+  ACT_HTANH = 2,     // clamp(x, 0, 20)                 (ERes2Net "ReLU" = nn.Hardtanh(0,20))
+  ACT_SILU = 3,      // x * sigmoid(x)
+  ACT_SIGMOID = 4,
+  ACT_TANH = 5,
+};
+
+// One input operand of the implicit GEMM, channels-last: element (img, h, w, c) lives at
+// p[((img*H + h)*W + w)*ld + c].  `cin` is the padded channel count the weights were packed
+// with (multiple of 4); channels cin_real..cin-1 must hold finite values (they meet zero
+// weights).  A 1-D (TDNN) tensor is H == 1.
+struct ConvSrc {
+  const float* p = nullptr;
+  const float* p2 = nullptr;   // optional addend with the same geometry (Res2Net "sp + spx")
+  int ld = 0, ld2 = 0;
+  int H = 1, W = 1;
+  int cin = 0;
+  int kh = 1, kw = 1, sh = 1, sw = 1, ph = 0, pw = 0, dh = 1, dw = 1;
+  int reflect = 0;             // speechbrain 'same' reflect padding (ECAPA Conv1d)
+};
+
+// out[m, n] = epi( sum_k A[m, k] * Wt[n, k] ), m = (img, ho, wo), k = (tap, c) of s0 then c of s1.
+struct ConvDesc {
+  ConvSrc s0, s1;              // s1 used only when s1.p != nullptr (1x1, K-concatenated)
+  int nimg = 0, Ho = 0, Wo = 0;
+  int N = 0;                   // output channels written (incl. zero padding columns)
+  int K = 0, Kp = 0;           // K = taps0*s0.cin + s1.cin ; Kp = round_up(K, 16)
+  const float* w = nullptr;    // [N][Kp]
+  const float* bias = nullptr; // [N] or null
+  float* out = nullptr; int ldo = 0;
+  int act = ACT_NONE;
+  const float* res = nullptr; int ldr = 0;             // added before act
+  const float* post_scale = nullptr;                   // after act: y*scale+shift (ECAPA BN after ReLU)
+  const float* post_shift = nullptr;
+  const float* affx = nullptr; int ldx = 0;            // AFF combine: x*(1+tanh v) + y*(1-tanh v)
+  const float* affy = nullptr; int ldy = 0;
+  const float* gate = nullptr; int gate_ld = 0; int gate_seg = 0;  // out *= gate[img][t/seg][n] (CAM)
+  int gate_nseg = 0;
+  int ksplit = 1; float* partial = nullptr;            // split-K partial slabs [ksplit][M][N]
+};
+
+hipError_t launch_conv(const ConvDesc& d, hipStream_t s);
+std::string conv_kernel_name(const ConvDesc& d);
+
+inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+}  // namespace spk

@@ -1,0 +1,334 @@
+// ERes2Net / ERes2NetV2 launch plan.
+//
+// Reference forwards: ERes2NetV2.py:65-91 (BasicBlockERes2NetV2), :132-159 (…AFF),
+// :235-254 (model); ERes2Net.py:61-87, :125-152, :208-231; fusion.py:22-28 (AFF);
+// pooling_layers.py:47-55 (TSTP).
+//
+// Data layout (workspace, channels-last [B, F, T, C]):
+//   * every block output is dense C = planes*expansion;
+//   * the conv1 output "T1" and the Res2Net concat buffer "CAT" hold `scale` slices of
+//     `width` channels, each zero-padded to a multiple of 4 (width 26 -> 28) so float4
+//     loads stay aligned; torch.split / torch.cat are just slice offsets;
+//   * conv3 + bn3 + shortcut conv + its BN + residual add + Hardtanh are ONE GEMM: the
+//     shortcut input is K-concatenated as a second operand with its own stride;
+//   * `sp + spx` is fused into the 3x3 conv's operand load; AFF is two GEMMs, the second
+//     applying x*(1+tanh a) + y*(1-tanh a) in its epilogue.
+#include <cmath>
+
+#include "misc.h"
+#include "runtime.h"
+
+namespace spk {
+
+namespace {
+
+struct T4 {
+  Buf buf;
+  int ld = 0, H = 0, W = 0, C = 0;   // C = physical channels
+};
+
+ConvSrc src_of(const Ctx*, const T4& t, int cin, int k, int stride, int pad) {
+  ConvSrc s;
+  s.ld = t.ld; s.H = t.H; s.W = t.W; s.cin = cin;
+  s.kh = s.kw = k; s.sh = s.sw = stride; s.ph = s.pw = pad;
+  return s;
+}
+
+int count_blocks(const Model& m, const std::string& layer) {
+  int n = 0;
+  while (m.has(layer + "." + std::to_string(n) + ".conv1.weight")) ++n;
+  return n;
+}
+
+struct ERes2Builder {
+  Builder& b;
+  Model& m;
+  bool v2;
+  int scale, expansion;
+  double base_width;
+  Buf T1, CAT, MID, FB;   // block scratch, sized for the largest layer
+
+  ERes2Builder(Builder& bb, bool isv2) : b(bb), m(bb.m), v2(isv2) {
+    scale = v2 ? m.cfg.scale : 2;
+    expansion = v2 ? m.cfg.expansion : 2;
+    base_width = v2 ? m.cfg.base_width : 32;
+    if (scale < 1 || expansion < 1) throw SpkError(SPK_E_INVALID, "bad scale/expansion");
+  }
+
+  double pix(const T4& t) const { return (double)t.H * t.W; }
+
+  // AFF(x, y) -> out (fusion.py:22-28); x, y, out share geometry, C logical channels each.
+  void aff(const std::string& p, const T4& x, const T4& y, int C, const T4& out) {
+    const int inter = C / 4;
+    const ChanMap xin = ChanMap::dense(C);
+    const int cp = xin.n_phys;
+    const ChanMap mid = ChanMap::dense(inter);
+    const Packed& a0 = m.pack(p + ".la0", mid,
+                              {Part{p + ".local_att.0.weight", p + ".local_att.0.bias", p + ".local_att.1", xin, 0, 0},
+                               Part{p + ".local_att.0.weight", "", "", xin, C, cp}},
+                              2 * cp);
+    const Packed& a1 = m.pack(p + ".la3", xin,
+                              {Part{p + ".local_att.3.weight", p + ".local_att.3.bias", p + ".local_att.4", mid, 0, 0}},
+                              mid.n_phys);
+    b.macs_per_utt += pix(x) * (2.0 * C * inter + (double)inter * C);
+    if (!b.plan) return;
+    ConvDesc d;
+    d.nimg = b.B; d.Ho = x.H; d.Wo = x.W;
+    d.s0 = src_of(nullptr, x, cp, 1, 1, 0);
+    d.s1 = src_of(nullptr, y, cp, 1, 1, 0);
+    d.ldo = mid.n_phys;
+    d.act = ACT_SILU;
+    Builder::ConvIO io;
+    io.s0 = x.buf; io.s1 = y.buf; io.out = MID;
+    b.conv(p + ".local_att.0", d, a0, io);
+    ConvDesc e;
+    e.nimg = b.B; e.Ho = x.H; e.Wo = x.W;
+    T4 midt{MID, mid.n_phys, x.H, x.W, mid.n_phys};
+    e.s0 = src_of(nullptr, midt, mid.n_phys, 1, 1, 0);
+    e.ldo = out.ld; e.ldx = x.ld; e.ldy = y.ld;
+    Builder::ConvIO io2;
+    io2.s0 = MID; io2.out = out.buf; io2.affx = x.buf; io2.affy = y.buf;
+    b.conv(p + ".local_att.3", e, a1, io2);
+  }
+
+  T4 block(const std::string& p, const T4& x, int stride, int width, int planes, bool use_aff, Buf outbuf) {
+    const int Ho = (x.H - 1) / stride + 1, Wo = (x.W - 1) / stride + 1;
+    const int Cout = planes * expansion;
+    const ChanMap sl = ChanMap::slices(width, scale);
+    const int wp = sl.n_phys / scale;
+    const int ldt = sl.n_phys;
+    const ChanMap xin = ChanMap::dense(x.C);
+    const double px = (double)Ho * Wo;
+
+    // conv1 (1x1, stride) + bn1 + Hardtanh -> T1 (scale slices)
+    const Packed& c1 = m.pack(p + ".conv1", sl, {Part{p + ".conv1.weight", "", p + ".bn1", xin, 0, 0}}, x.C);
+    b.macs_per_utt += px * x.C * (double)width * scale;
+    if (b.plan) {
+      ConvDesc d;
+      d.nimg = b.B; d.Ho = Ho; d.Wo = Wo;
+      d.s0 = src_of(nullptr, x, x.C, 1, stride, 0);
+      d.ldo = ldt; d.act = ACT_HTANH;
+      Builder::ConvIO io; io.s0 = x.buf; io.out = T1;
+      b.conv(p + ".conv1", d, c1, io);
+    }
+    const T4 t1{T1, ldt, Ho, Wo, ldt};
+    const T4 cat{CAT, ldt, Ho, Wo, ldt};
+    for (int i = 0; i < scale; ++i) {
+      T4 in{T1.at((size_t)i * wp), ldt, Ho, Wo, wp};
+      Buf addend;
+      int add_ld = 0;
+      if (i > 0) {
+        T4 prev{CAT.at((size_t)(i - 1) * wp), ldt, Ho, Wo, wp};
+        if (use_aff) {
+          T4 f{FB, wp, Ho, Wo, wp};
+          aff(p + ".fuse_models." + std::to_string(i - 1), prev, in, width, f);
+          in = f;
+        } else {
+          addend = prev.buf;
+          add_ld = ldt;
+        }
+      }
+      const ChanMap one = ChanMap::dense(width);
+      const std::string ci = std::to_string(i);
+      const Packed& cv = m.pack(p + ".convs." + ci, one,
+                                {Part{p + ".convs." + ci + ".weight", "", p + ".bns." + ci, one, 0, 0}}, 9 * wp);
+      b.macs_per_utt += px * 9.0 * width * width;
+      if (b.plan) {
+        ConvDesc d;
+        d.nimg = b.B; d.Ho = Ho; d.Wo = Wo;
+        d.s0 = src_of(nullptr, in, wp, 3, 1, 1);
+        if (addend) d.s0.ld2 = add_ld;
+        d.ldo = ldt; d.act = ACT_HTANH;
+        Builder::ConvIO io; io.s0 = in.buf; io.s0b = addend; io.out = CAT.at((size_t)i * wp);
+        b.conv(p + ".convs." + ci, d, cv, io);
+      }
+    }
+    // conv3 + bn3 (+ shortcut conv + bn, K-concatenated) + residual + Hardtanh
+    const bool has_sc = m.has(p + ".shortcut.0.weight");
+    const ChanMap om = ChanMap::dense(Cout);
+    std::vector<Part> parts{Part{p + ".conv3.weight", "", p + ".bn3", sl, 0, 0}};
+    int K = ldt;
+    if (has_sc) {
+      parts.push_back(Part{p + ".shortcut.0.weight", "", p + ".shortcut.1", xin, 0, ldt});
+      K += x.C;
+    } else if (stride != 1 || x.C != Cout) {
+      throw SpkError(SPK_E_WEIGHTS, p + ": missing shortcut for a shape-changing block");
+    }
+    const Packed& c3 = m.pack(p + ".conv3", om, parts, K);
+    b.macs_per_utt += px * (double)width * scale * Cout + (has_sc ? px * x.C * (double)Cout : 0.0);
+    T4 out{outbuf, om.n_phys, Ho, Wo, om.n_phys};
+    if (b.plan) {
+      ConvDesc d;
+      d.nimg = b.B; d.Ho = Ho; d.Wo = Wo;
+      d.s0 = src_of(nullptr, cat, ldt, 1, 1, 0);
+      Builder::ConvIO io; io.s0 = CAT; io.out = outbuf;
+      if (has_sc) {
+        d.s1 = src_of(nullptr, x, x.C, 1, stride, 0);
+        io.s1 = x.buf;
+      } else {
+        d.ldr = x.ld;
+        io.res = x.buf;
+      }
+      d.ldo = out.ld; d.act = ACT_HTANH;
+      b.conv(p + ".conv3", d, c3, io);
+    }
+    return out;
+  }
+
+  void run(int T) {
+    const int B = b.B;
+    const int F = m.cfg.feat_dim;
+    const int mc = m.cfg.m_channels;
+    if (mc % 4) throw SpkError(SPK_E_UNSUPPORTED, "m_channels must be a multiple of 4");
+    // ---- stem conv 3x3 1->mc + bn1 + relu (ERes2NetV2.py:238)
+    const Packed& stem = m.pack("conv1", ChanMap::dense(mc), {Part{"conv1.weight", "", "bn1", ChanMap::dense(1, 1), 0, 0}}, 9);
+    T4 x{b.alloc((size_t)B * F * T * mc), mc, F, T, mc};
+    b.macs_per_utt += (double)F * T * mc * 9;
+    if (b.plan) {
+      const float* w = m.dptr(stem.w_off);
+      const float* bias = m.dptr(stem.b_off);
+      const int kp = stem.Kp;
+      const Buf xo = x.buf;
+      const int ld = x.ld;
+      b.step("stem", [=](const Ctx& c) {
+        return launch_stem_conv3x3(c.in, B, T, F, w, bias, mc, ACT_RELU, kp, c.resolve(xo), ld, c.stream);
+      });
+    }
+    // ---- scratch for the block internals, sized by the largest layer
+    size_t t1_max = 0, mid_max = 0, fb_max = 0;
+    {
+      int H = F, W = T;
+      for (int li = 0; li < 4; ++li) {
+        const int stride = li ? 2 : 1;
+        H = (H - 1) / stride + 1; W = (W - 1) / stride + 1;
+        const int width = (int)std::floor((mc << li) * (base_width / 64.0));
+        const size_t px = (size_t)B * H * W;
+        t1_max = std::max(t1_max, px * ChanMap::slices(width, scale).n_phys);
+        mid_max = std::max(mid_max, px * ChanMap::dense(width / 4).n_phys);
+        fb_max = std::max(fb_max, px * ChanMap::dense(width).n_phys);
+        const int C = (mc << li) * expansion;   // model-level AFF at this resolution
+        mid_max = std::max(mid_max, px * ChanMap::dense(C / 4).n_phys);
+      }
+    }
+    T1 = b.alloc(t1_max);
+    CAT = b.alloc(t1_max);
+    MID = b.alloc(mid_max);
+    FB = b.alloc(fb_max);
+
+    T4 outs[4];
+    for (int li = 0; li < 4; ++li) {
+      const std::string layer = "layer" + std::to_string(li + 1);
+      const int planes = mc << li;
+      const int width = (int)std::floor(planes * (base_width / 64.0));
+      const int stride = li ? 2 : 1;
+      const int nb = count_blocks(m, layer);
+      if (nb == 0) throw SpkError(SPK_E_WEIGHTS, "no blocks in " + layer);
+      const int Ho = (x.H - 1) / stride + 1, Wo = (x.W - 1) / stride + 1;
+      const size_t osz = (size_t)B * Ho * Wo * ChanMap::dense(planes * expansion).n_phys;
+      Buf pp[2] = {b.alloc(osz), b.alloc(osz)};
+      for (int bi = 0; bi < nb; ++bi)
+        x = block(layer + "." + std::to_string(bi), x, bi ? 1 : stride, width, planes, li >= 2, pp[bi & 1]);
+      outs[li] = x;
+    }
+
+    T4 fused;
+    auto downsample = [&](const std::string& key, const T4& in) {
+      const int Cout = (int)m.dim(key, 0);
+      const ChanMap om = ChanMap::dense(Cout);
+      const Packed& p = m.pack(key, om, {Part{key, "", "", ChanMap::dense(in.C), 0, 0}}, 9 * in.C);
+      const int Ho = (in.H - 1) / 2 + 1, Wo = (in.W - 1) / 2 + 1;
+      T4 out{b.alloc((size_t)B * Ho * Wo * om.n_phys), om.n_phys, Ho, Wo, om.n_phys};
+      b.macs_per_utt += (double)Ho * Wo * Cout * in.C * 9.0;
+      if (b.plan) {
+        ConvDesc d;
+        d.nimg = B; d.Ho = Ho; d.Wo = Wo;
+        d.s0 = src_of(nullptr, in, in.C, 3, 2, 1);
+        d.ldo = out.ld;
+        Builder::ConvIO io; io.s0 = in.buf; io.out = out.buf;
+        b.conv(key, d, p, io, /*use_bias=*/false);
+      }
+      return out;
+    };
+    auto fuse = [&](const std::string& key, const T4& a, const T4& y) {
+      T4 out{b.alloc((size_t)B * a.H * a.W * a.C), a.C, a.H, a.W, a.C};
+      aff(key, a, y, a.C, out);
+      return out;
+    };
+    if (v2) {
+      const T4 ds = downsample("layer3_ds.weight", outs[2]);
+      fused = fuse("fuse34", outs[3], ds);
+    } else {
+      const T4 d1 = downsample("layer1_downsample.weight", outs[0]);
+      const T4 f12 = fuse("fuse_mode12", outs[1], d1);
+      const T4 d2 = downsample("layer2_downsample.weight", f12);
+      const T4 f123 = fuse("fuse_mode123", outs[2], d2);
+      const T4 d3 = downsample("layer3_downsample.weight", f123);
+      fused = fuse("fuse_mode1234", outs[3], d3);
+    }
+
+    // ---- TSTP (pooling_layers.py:47-55) -> stats [B, 2*H*C] in (h, c) order
+    const int H4 = fused.H, C4 = fused.C;
+    const int S = 2 * H4 * C4;
+    const Buf stats = b.alloc((size_t)B * S);
+    if (b.plan) {
+      const T4 f = fused;
+      b.step("pool", [=](const Ctx& c) {
+        return launch_tstp(c.resolve(f.buf), B, f.H, f.W, f.C, f.ld, 1e-8f, 1, c.resolve(stats), c.stream);
+      });
+    }
+    // reference flattens (C, F): index c*H + h  -> our h*C + c
+    ChanMap perm;
+    perm.phys.resize(S);
+    perm.n_phys = S;
+    for (int part = 0; part < 2; ++part)
+      for (int c = 0; c < C4; ++c)
+        for (int h = 0; h < H4; ++h) perm.phys[part * H4 * C4 + c * H4 + h] = part * H4 * C4 + h * C4 + c;
+    const int E = (int)m.dim("seg_1.weight", 0);
+    if (E % 4) throw SpkError(SPK_E_UNSUPPORTED, "embedding_size must be a multiple of 4");
+    if (m.dim("seg_1.weight", 1) != S) throw SpkError(SPK_E_WEIGHTS, "seg_1 in_features != pooled stats size");
+    const bool two = m.cfg.two_emb_layer != 0;
+    const ChanMap em = ChanMap::dense(E, 1);
+    const Packed& seg1 = m.pack("seg_1", em, {Part{"seg_1.weight", "seg_1.bias", "", perm, 0, 0}}, S);
+    b.macs_per_utt += (double)S * E;
+    const T4 st{stats, S, 1, 1, S};
+    Buf e1 = two ? b.alloc((size_t)B * E) : Buf{Buf::OUT, 0, nullptr};
+    if (b.plan) {
+      ConvDesc d;
+      d.nimg = B; d.Ho = 1; d.Wo = 1;
+      d.s0 = src_of(nullptr, st, S, 1, 1, 0);
+      d.ldo = E;
+      if (two) {
+        const Packed& pa = m.pack_post_affine("seg_bn_1", "seg_bn_1", em);
+        d.act = ACT_RELU;
+        d.post_scale = m.dptr(pa.ps_off);
+        d.post_shift = m.dptr(pa.pt_off);
+      }
+      Builder::ConvIO io; io.s0 = stats; io.out = e1;
+      b.conv("seg_1", d, seg1, io);
+    } else if (two) {
+      m.pack_post_affine("seg_bn_1", "seg_bn_1", em);
+    }
+    if (two) {
+      const Packed& seg2 = m.pack("seg_2", em, {Part{"seg_2.weight", "seg_2.bias", "", ChanMap::dense(E, 1), 0, 0}}, E);
+      b.macs_per_utt += (double)E * E;
+      if (b.plan) {
+        ConvDesc d;
+        d.nimg = B; d.Ho = 1; d.Wo = 1;
+        const T4 t{e1, E, 1, 1, E};
+        d.s0 = src_of(nullptr, t, E, 1, 1, 0);
+        d.ldo = E;
+        Builder::ConvIO io; io.s0 = e1; io.out = Buf{Buf::OUT, 0, nullptr};
+        b.conv("seg_2", d, seg2, io);
+      }
+    }
+  }
+};
+
+}  // namespace
+
+void build_eres2net(Builder& b, int T, bool v2) {
+  ERes2Builder eb(b, v2);
+  eb.run(T);
+}
+
+}  // namespace spk

@@ -1,0 +1,24 @@
+// Fbank tables + launcher (see fbank.hip).
+#pragma once
+#include "common.h"
+
+namespace spk {
+
+struct FbankTables {
+  float window[400];        // Povey window hann(400, periodic=False)^0.85
+  float2 twiddle[256];      // exp(-2 pi i k / 512)
+  int mel_start[128];       // first FFT bin of filter m
+  int mel_len[128];         // number of bins with non-zero weight
+  int mel_off[128];         // offset of its weights in mel_w
+  float mel_w[4096];
+};
+
+// Host-side construction (double precision, rounded once to float).  Returns the number
+// of mel weights used; -1 if n_mels is unsupported.
+int build_fbank_tables(FbankTables* t, int n_mels, double sample_rate);
+
+hipError_t launch_fbank(const float* wav, const int64_t* wav_off, int n_utt, float* feats,
+                        const int64_t* frame_off, int n_mels, int mean_nor, const FbankTables* tab,
+                        hipStream_t s);
+
+}  // namespace spk

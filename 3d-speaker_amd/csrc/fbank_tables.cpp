@@ -1,0 +1,52 @@
+// Host construction of the Fbank constant tables (double precision, rounded once).
+// Window: torchaudio _feature_window_function(POVEY) = hann_window(400, periodic=False)^0.85.
+// Mel bank: torchaudio get_mel_banks (mel = 1127 ln(1 + f/700), low 20 Hz, high = Nyquist,
+// 512-point FFT, vtln_warp = 1), the Nyquist column is zero so only bins 0..255 carry weight.
+#include <cmath>
+#include "fbank.h"
+
+namespace spk {
+
+int build_fbank_tables(FbankTables* t, int n_mels, double sample_rate) {
+  if (n_mels <= 3 || n_mels > 128) return -1;
+  const double pi = 3.14159265358979323846;
+  for (int i = 0; i < 400; ++i) {
+    const double h = 0.5 - 0.5 * std::cos(2.0 * pi * i / 399.0);
+    t->window[i] = (float)std::pow(h, 0.85);
+  }
+  for (int k = 0; k < 256; ++k) {
+    const double a = -2.0 * pi * k / 512.0;
+    t->twiddle[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+  }
+  auto mel = [](double f) { return 1127.0 * std::log(1.0 + f / 700.0); };
+  const double nyq = 0.5 * sample_rate;
+  const double bin_w = sample_rate / 512.0;
+  const double mlo = mel(20.0), mhi = mel(nyq);
+  const double delta = (mhi - mlo) / (n_mels + 1);
+  int off = 0;
+  for (int m = 0; m < n_mels; ++m) {
+    const double left = mlo + m * delta, center = mlo + (m + 1) * delta, right = mlo + (m + 2) * delta;
+    int first = -1, last = -1;
+    for (int b = 0; b < 256; ++b) {
+      const double mb = mel(bin_w * b);
+      const double w = std::fmax(0.0, std::fmin((mb - left) / (center - left), (right - mb) / (right - center)));
+      if (w > 0.0) {
+        if (first < 0) first = b;
+        last = b;
+      }
+    }
+    if (first < 0) { first = 0; last = -1; }
+    t->mel_start[m] = first;
+    t->mel_len[m] = last - first + 1;
+    t->mel_off[m] = off;
+    for (int b = first; b <= last; ++b) {
+      const double mb = mel(bin_w * b);
+      const double w = std::fmax(0.0, std::fmin((mb - left) / (center - left), (right - mb) / (right - center)));
+      if (off >= 4096) return -1;
+      t->mel_w[off++] = (float)w;
+    }
+  }
+  return off;
+}
+
+}  // namespace spk

@@ -1,0 +1,12 @@
+#pragma once
+#include <algorithm>
+#include "common.h"
+
+namespace spk {
+
+hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const float* w, const float* bias, int cout,
+                               int act, int wstride, float* out, int ldo, hipStream_t s);
+hipError_t launch_tstp(const float* x, int B, int H, int W, int C, int ld, float eps, int unbiased, float* out,
+                       hipStream_t s);
+
+}  // namespace spk

@@ -1,0 +1,98 @@
+// Small bandwidth-bound kernels around the implicit-GEMM convs, gfx950:
+//  * stem conv 3x3, 1 -> Cout channels, reading Fbank features [B, T, F] directly (the
+//    reference's permute(0,2,1).unsqueeze(1) is folded into the index math), folded BN
+//    and ReLU in the epilogue, channels-last output (ERes2NetV2.py:236-238, DTDNN.py:40-41);
+//  * TSTP statistics pooling (pooling_layers.py:47-55): mean and sqrt(unbiased var+1e-8)
+//    over time per (freq, channel), one lane per channel so loads are coalesced;
+//  * CAM++ StatsPool (layers.py:26-37: mean and unbiased std, no eps).
+#include "common.h"
+#include "misc.h"
+
+namespace spk {
+
+namespace {
+
+__global__ void __launch_bounds__(256)
+stem_conv3x3_kernel(const float* __restrict__ feats, int B, int T, int F, const float* __restrict__ w,
+                    const float* __restrict__ bias, int cout, int act, int wstride, float* __restrict__ out,
+                    int ldo) {
+  // thread -> (pixel, 4 output channels); pixel = (b, f, t) of the (F, T) image
+  const int groups = cout / 4;
+  const long long total = (long long)B * F * T * groups;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int g = (int)(e % groups);
+    const long long pix = e / groups;
+    const int t = (int)(pix % T);
+    const int f = (int)((pix / T) % F);
+    const int b = (int)(pix / ((long long)T * F));
+    float in[9];
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const int ff = f + dy - 1, tt = t + dx - 1;
+        in[dy * 3 + dx] = (ff >= 0 && ff < F && tt >= 0 && tt < T) ? feats[((size_t)b * T + tt) * F + ff] : 0.f;
+      }
+    float4 o;
+    float* op = &o.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = g * 4 + j;
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc = fmaf(in[k], w[c * wstride + k], acc);
+      acc += bias[c];
+      op[j] = act == ACT_RELU ? fmaxf(acc, 0.f) : acc;
+    }
+    *reinterpret_cast<float4*>(out + pix * ldo + g * 4) = o;
+  }
+}
+
+// x: [B, H, W, C] (pixel stride ld).  out: [B, 2*H*C]: mean at [h*C + c], std at [H*C + h*C + c].
+__global__ void __launch_bounds__(256)
+tstp_kernel(const float* __restrict__ x, int B, int H, int W, int C, int ld, float eps, int unbiased,
+            float* __restrict__ out) {
+  const long long total = (long long)B * H * C;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const int h = (int)((e / C) % H);
+    const int b = (int)(e / ((long long)C * H));
+    const float* p = x + ((size_t)(b * H + h) * W) * ld + c;
+    float s = 0.f;
+    for (int t = 0; t < W; ++t) s += p[(size_t)t * ld];
+    const float mean = s / (float)W;
+    float q = 0.f;
+    for (int t = 0; t < W; ++t) {
+      const float dlt = p[(size_t)t * ld] - mean;
+      q = fmaf(dlt, dlt, q);
+    }
+    const float var = q / (float)(unbiased ? W - 1 : W);
+    float* o = out + (size_t)b * 2 * H * C;
+    o[h * C + c] = mean;
+    o[H * C + h * C + c] = sqrtf(var + eps);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const float* w, const float* bias, int cout,
+                               int act, int wstride, float* out, int ldo, hipStream_t s) {
+  if (cout % 4 || ldo % 4) return hipErrorInvalidValue;
+  const long long total = (long long)B * F * T * (cout / 4);
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 65536);
+  hipLaunchKernelGGL(stem_conv3x3_kernel, dim3(blocks), dim3(256), 0, s, feats, B, T, F, w, bias, cout, act, wstride, out,
+                     ldo);
+  return hipGetLastError();
+}
+
+hipError_t launch_tstp(const float* x, int B, int H, int W, int C, int ld, float eps, int unbiased, float* out,
+                       hipStream_t s) {
+  const long long total = (long long)B * H * C;
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 65536);
+  hipLaunchKernelGGL(tstp_kernel, dim3(blocks), dim3(256), 0, s, x, B, H, W, C, ld, eps, unbiased, out);
+  return hipGetLastError();
+}
+
+}  // namespace spk

@@ -1,0 +1,456 @@
+// libspk_hip C ABI + executor core (weight folding/packing, plans, workspace).
+#include "runtime.h"
+
+#include <cmath>
+#include <cstring>
+
+#include "fbank.h"
+#include "misc.h"
+
+namespace spk {
+
+thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+ChanMap ChanMap::dense(int c, int align) {
+  ChanMap m;
+  m.phys.resize(c);
+  for (int i = 0; i < c; ++i) m.phys[i] = i;
+  m.n_phys = round_up(c, align);
+  return m;
+}
+
+ChanMap ChanMap::slices(int width, int n, int align) {
+  ChanMap m;
+  const int wp = round_up(width, align);
+  m.phys.resize((size_t)width * n);
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < width; ++i) m.phys[(size_t)j * width + i] = j * wp + i;
+  m.n_phys = wp * n;
+  return m;
+}
+
+const Model::HostT& Model::get(const std::string& k) const {
+  auto it = W.find(k);
+  if (it == W.end()) throw SpkError(SPK_E_WEIGHTS, "missing state_dict tensor: " + k);
+  return it->second;
+}
+
+int64_t Model::dim(const std::string& k, int i) const {
+  auto it = shapes.find(k);
+  if (it == shapes.end()) throw SpkError(SPK_E_WEIGHTS, "missing state_dict tensor: " + k);
+  if (i >= (int)it->second.size()) throw SpkError(SPK_E_WEIGHTS, "rank too small: " + k);
+  return it->second[i];
+}
+
+size_t Model::put(const std::vector<float>& v) {
+  const size_t off = (arena.size() + 63) / 64 * 64;
+  arena.resize(off + v.size());
+  std::memcpy(arena.data() + off, v.data(), v.size() * sizeof(float));
+  return off;
+}
+
+void Model::bn_fold(const std::string& bn, int n, std::vector<double>& s, std::vector<double>& t, double eps) const {
+  s.assign(n, 1.0);
+  t.assign(n, 0.0);
+  if (bn.empty()) return;
+  const HostT& mean = get(bn + ".running_mean");
+  const HostT& var = get(bn + ".running_var");
+  if ((int)mean.data.size() != n || (int)var.data.size() != n)
+    throw SpkError(SPK_E_WEIGHTS, bn + ": BatchNorm size mismatch");
+  const HostT* g = W.count(bn + ".weight") ? &get(bn + ".weight") : nullptr;
+  const HostT* be = W.count(bn + ".bias") ? &get(bn + ".bias") : nullptr;
+  for (int c = 0; c < n; ++c) {
+    const double gamma = g ? g->data[c] : 1.0;
+    const double beta = be ? be->data[c] : 0.0;
+    s[c] = gamma / std::sqrt((double)var.data[c] + eps);
+    t[c] = beta - (double)mean.data[c] * s[c];
+  }
+}
+
+const Packed& Model::pack(const std::string& name, const ChanMap& out, const std::vector<Part>& parts, int K) {
+  auto it = packed.find(name);
+  if (it != packed.end()) return it->second;
+  if (uploaded) throw SpkError(SPK_E_INVALID, "internal: pack after upload: " + name);
+  const int N = out.n_phys;
+  const int Kp = round_up(K, 16);
+  std::vector<double> wd((size_t)N * Kp, 0.0), bd(N, 0.0);
+  std::map<std::string, int> seen;
+  bool has_bias = false;
+  for (const Part& part : parts) {
+    const HostT& w = get(part.wkey);
+    if (w.shape.size() < 2) throw SpkError(SPK_E_WEIGHTS, part.wkey + ": expected a conv/linear weight");
+    const int cout = (int)w.shape[0], cin = (int)w.shape[1];
+    int taps = 1;
+    for (size_t i = 2; i < w.shape.size(); ++i) taps *= (int)w.shape[i];
+    if (cout != out.n_log()) throw SpkError(SPK_E_WEIGHTS, part.wkey + ": out channels mismatch");
+    const int nin = part.in.n_log(), cinp = part.in.n_phys;
+    if (part.ci_lo + nin > cin) throw SpkError(SPK_E_WEIGHTS, part.wkey + ": in channels mismatch");
+    if (part.kofs + taps * cinp > K) throw SpkError(SPK_E_INVALID, "internal: K overflow packing " + part.wkey);
+    std::vector<double> s, t;
+    bn_fold(part.bn, cout, s, t);
+    const bool first = seen.count(part.wkey) == 0;
+    seen[part.wkey] = 1;
+    for (int co = 0; co < cout; ++co) {
+      double* row = wd.data() + (size_t)out.phys[co] * Kp + part.kofs;
+      const float* src = w.data.data() + (size_t)co * cin * taps;
+      for (int ci = 0; ci < nin; ++ci)
+        for (int tap = 0; tap < taps; ++tap)
+          row[(size_t)tap * cinp + part.in.phys[ci]] = (double)src[(size_t)(part.ci_lo + ci) * taps + tap] * s[co];
+    }
+    if (first) {
+      const HostT* cb = part.bias_key.empty() ? nullptr : &get(part.bias_key);
+      if (cb || !part.bn.empty()) has_bias = true;
+      for (int co = 0; co < cout; ++co) bd[out.phys[co]] += (cb ? s[co] * cb->data[co] : 0.0) + t[co];
+    }
+  }
+  Packed p;
+  p.N = N; p.K = K; p.Kp = Kp; p.has_bias = has_bias;
+  std::vector<float> wf(wd.begin(), wd.end()), bf(bd.begin(), bd.end());
+  p.w_off = put(wf);
+  p.b_off = put(bf);
+  return packed.emplace(name, p).first->second;
+}
+
+const Packed& Model::pack_post_affine(const std::string& name, const std::string& bn, const ChanMap& out) {
+  const std::string key = name + "#post";
+  auto it = packed.find(key);
+  if (it != packed.end()) return it->second;
+  if (uploaded) throw SpkError(SPK_E_INVALID, "internal: pack after upload: " + key);
+  std::vector<double> s, t;
+  bn_fold(bn, out.n_log(), s, t);
+  std::vector<float> ps(out.n_phys, 0.f), pt(out.n_phys, 0.f);
+  for (int c = 0; c < out.n_log(); ++c) { ps[out.phys[c]] = (float)s[c]; pt[out.phys[c]] = (float)t[c]; }
+  Packed p;
+  p.N = out.n_phys;
+  p.ps_off = put(ps);
+  p.pt_off = put(pt);
+  return packed.emplace(key, p).first->second;
+}
+
+Buf Builder::alloc(size_t floats) {
+  Buf b;
+  b.kind = Buf::WS;
+  b.off = ws;
+  ws += (floats * sizeof(float) + 255) / 256 * 256;
+  return b;
+}
+
+void Builder::step(const std::string& name, Step s, const std::string& kernel) {
+  if (!plan) return;
+  plan->steps.push_back(std::move(s));
+  plan->names.push_back(name);
+  plan->kernels.push_back(kernel.empty() ? name : kernel);
+  plan->flops.push_back(2.0 * (macs_per_utt - macs_at_last_step) * B);
+  macs_at_last_step = macs_per_utt;
+}
+
+void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const ConvIO& io, bool use_bias) {
+  if (!plan) return;
+  d.N = p.N; d.K = p.K; d.Kp = p.Kp;
+  d.w = m.dptr(p.w_off);
+  d.bias = (use_bias && p.has_bias) ? m.dptr(p.b_off) : nullptr;
+  const int M = d.nimg * d.Ho * d.Wo;
+  // split-K for skinny, deep GEMMs (e.g. the 20480 -> 192 embedding layer)
+  const int bm = d.N <= 32 ? 256 : (d.N <= 64 ? 128 : (M <= 4096 ? 64 : 128));
+  const int bn = d.N <= 32 ? 32 : (d.N <= 64 ? 64 : 128);
+  const int nblk = ((M + bm - 1) / bm) * ((d.N + bn - 1) / bn);
+  const int nkt = d.Kp / 16;
+  Buf partial;
+  if (nblk < 128 && nkt >= 64 && !io.affx && !io.gate) {
+    d.ksplit = std::max(1, std::min(nkt / 16, (256 + nblk - 1) / nblk));
+    if (d.ksplit > 1) partial = alloc((size_t)d.ksplit * M * d.N);
+  }
+  ConvIO cio = io;
+  cio.partial = partial;
+  ConvDesc probe = d;   // kernel label: same tile choice as launch_conv
+  probe.s1.cin = io.s1 ? d.s1.cin : 0;
+  probe.s0.ld2 = io.s0b ? std::max(d.s0.ld2, 1) : 0;
+  step(name, [d, cio](const Ctx& c) mutable {
+    d.s0.p = c.resolve(cio.s0);
+    d.s0.p2 = c.resolve(cio.s0b);
+    d.s1.p = c.resolve(cio.s1);
+    d.out = c.resolve(cio.out);
+    d.res = c.resolve(cio.res);
+    d.affx = c.resolve(cio.affx);
+    d.affy = c.resolve(cio.affy);
+    d.gate = c.resolve(cio.gate);
+    d.partial = c.resolve(cio.partial);
+    return launch_conv(d, c.stream);
+  }, conv_kernel_name(probe));
+}
+
+}  // namespace spk
+
+// ============================================================================ C ABI
+using namespace spk;
+
+struct spk_model {
+  Model m;
+};
+
+namespace {
+
+FbankTables* g_tables[64] = {nullptr};
+int g_tables_mels[64] = {0};
+std::mutex g_tables_mu;
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const SpkError& e) {
+    set_error(e.what());
+    return e.code;
+  } catch (const std::exception& e) {
+    set_error(std::string("internal error: ") + e.what());
+    return SPK_E_INVALID;
+  }
+}
+
+int hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return SPK_OK;
+  set_error(std::string(what) + ": " + hipGetErrorString(e));
+  return SPK_E_HIP;
+}
+
+Plan* get_plan(spk_model_t* h, int B, int T, double* macs = nullptr) {
+  std::lock_guard<std::mutex> lk(h->m.mu);
+  auto key = std::make_pair(B, T);
+  auto it = h->m.plans.find(key);
+  if (it != h->m.plans.end()) return it->second.get();
+  auto plan = std::make_unique<Plan>();
+  Builder b(h->m, plan.get(), B);
+  switch (h->m.cfg.arch) {
+    case SPK_ARCH_ERES2NETV2: build_eres2net(b, T, true); break;
+    case SPK_ARCH_ERES2NET: build_eres2net(b, T, false); break;
+    case SPK_ARCH_ECAPA: build_ecapa(b, T); break;
+    case SPK_ARCH_CAMPPLUS: build_campplus(b, T); break;
+    default: throw SpkError(SPK_E_UNSUPPORTED, "unknown arch");
+  }
+  plan->ws_bytes = b.ws;
+  (void)macs;
+  Plan* p = plan.get();
+  h->m.plans.emplace(key, std::move(plan));
+  return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+int spk_version(void) { return 1; }
+
+const char* spk_last_error(void) { return g_last_error.c_str(); }
+
+int spk_fbank_f32(const float* wav, const int64_t* wav_offsets, int32_t n_utt, float* feats,
+                  const int64_t* frame_offsets, int32_t n_mels, int32_t mean_nor, void* stream) {
+  return guarded([&]() -> int {
+    if (n_utt < 0 || n_mels <= 3 || n_mels > 128 || (n_utt > 0 && (!wav || !wav_offsets || !feats || !frame_offsets))) {
+      set_error("spk_fbank_f32: invalid argument");
+      return SPK_E_INVALID;
+    }
+    int dev = 0;
+    if (int rc = hip_check(hipGetDevice(&dev), "hipGetDevice")) return rc;
+    if (dev < 0 || dev >= 64) return SPK_E_DEVICE;
+    FbankTables* tab = nullptr;
+    {
+      std::lock_guard<std::mutex> lk(g_tables_mu);
+      if (!g_tables[dev] || g_tables_mels[dev] != n_mels) {
+        FbankTables host;
+        std::memset(&host, 0, sizeof(host));
+        if (build_fbank_tables(&host, n_mels, 16000.0) < 0) {
+          set_error("spk_fbank_f32: unsupported n_mels");
+          return SPK_E_UNSUPPORTED;
+        }
+        if (!g_tables[dev]) {
+          if (int rc = hip_check(hipMalloc(&g_tables[dev], sizeof(FbankTables)), "hipMalloc(fbank tables)")) return rc;
+        }
+        if (int rc = hip_check(hipMemcpy(g_tables[dev], &host, sizeof(host), hipMemcpyHostToDevice), "hipMemcpy"))
+          return rc;
+        g_tables_mels[dev] = n_mels;
+      }
+      tab = g_tables[dev];
+    }
+    return hip_check(launch_fbank(wav, wav_offsets, n_utt, feats, frame_offsets, n_mels, mean_nor, tab,
+                                  reinterpret_cast<hipStream_t>(stream)),
+                     "fbank launch");
+  });
+}
+
+int spk_model_create(const spk_model_config_t* cfg, const spk_weight_t* weights, int32_t n_weights, spk_model_t** out) {
+  return guarded([&]() -> int {
+    if (!cfg || !out || (n_weights > 0 && !weights)) {
+      set_error("spk_model_create: null argument");
+      return SPK_E_INVALID;
+    }
+    auto h = std::make_unique<spk_model>();
+    h->m.cfg = *cfg;
+    if (int rc = hip_check(hipGetDevice(&h->m.device), "hipGetDevice")) return rc;
+    for (int i = 0; i < n_weights; ++i) {
+      const spk_weight_t& w = weights[i];
+      if (!w.name || w.ndim < 0 || w.ndim > 4) {
+        set_error("spk_model_create: bad weight descriptor");
+        return SPK_E_INVALID;
+      }
+      std::vector<int64_t> shape(w.shape, w.shape + w.ndim);
+      h->m.shapes[w.name] = shape;
+      if (!w.data) continue;
+      size_t n = 1;
+      for (auto d : shape) n *= (size_t)d;
+      Model::HostT t;
+      t.shape = shape;
+      t.data.assign(w.data, w.data + n);
+      h->m.W[w.name] = std::move(t);
+    }
+    // pack every layer (a plan-less build), then upload once
+    {
+      Builder b(h->m, nullptr, 1);
+      switch (cfg->arch) {
+        case SPK_ARCH_ERES2NETV2: build_eres2net(b, 200, true); break;
+        case SPK_ARCH_ERES2NET: build_eres2net(b, 200, false); break;
+        case SPK_ARCH_ECAPA: build_ecapa(b, 200); break;
+        case SPK_ARCH_CAMPPLUS: build_campplus(b, 200); break;
+        default: set_error("spk_model_create: unknown arch"); return SPK_E_UNSUPPORTED;
+      }
+    }
+    h->m.dweights_bytes = h->m.arena.size() * sizeof(float);
+    if (int rc = hip_check(hipMalloc(&h->m.dweights, std::max<size_t>(h->m.dweights_bytes, 256)), "hipMalloc(weights)"))
+      return rc;
+    if (int rc = hip_check(hipMemcpy(h->m.dweights, h->m.arena.data(), h->m.dweights_bytes, hipMemcpyHostToDevice),
+                           "hipMemcpy(weights)")) {
+      (void)hipFree(h->m.dweights);
+      return rc;
+    }
+    h->m.uploaded = true;
+    h->m.arena.clear();
+    h->m.arena.shrink_to_fit();
+    h->m.W.clear();
+    *out = h.release();
+    return SPK_OK;
+  });
+}
+
+int spk_model_destroy(spk_model_t* model) {
+  if (!model) return SPK_OK;
+  if (model->m.dweights) (void)hipFree(model->m.dweights);
+  delete model;
+  return SPK_OK;
+}
+
+int spk_model_workspace_bytes(spk_model_t* model, int32_t B, int32_t T, size_t* bytes) {
+  return guarded([&]() -> int {
+    if (!model || !bytes || B <= 0 || T <= 0) {
+      set_error("spk_model_workspace_bytes: invalid argument");
+      return SPK_E_INVALID;
+    }
+    *bytes = get_plan(model, B, T)->ws_bytes;
+    return SPK_OK;
+  });
+}
+
+int spk_model_flops(spk_model_t* model, int32_t T, double* flops) {
+  return guarded([&]() -> int {
+    if (!model || !flops || T <= 0) {
+      set_error("spk_model_flops: invalid argument");
+      return SPK_E_INVALID;
+    }
+    Builder b(model->m, nullptr, 1);
+    switch (model->m.cfg.arch) {
+      case SPK_ARCH_ERES2NETV2: build_eres2net(b, T, true); break;
+      case SPK_ARCH_ERES2NET: build_eres2net(b, T, false); break;
+      case SPK_ARCH_ECAPA: build_ecapa(b, T); break;
+      case SPK_ARCH_CAMPPLUS: build_campplus(b, T); break;
+      default: return SPK_E_UNSUPPORTED;
+    }
+    *flops = 2.0 * b.macs_per_utt;
+    return SPK_OK;
+  });
+}
+
+int spk_model_forward(spk_model_t* model, const float* feats, int32_t B, int32_t T, void* workspace,
+                      size_t workspace_bytes, float* emb_out, void* stream) {
+  return guarded([&]() -> int {
+    if (!model || !feats || !emb_out || B <= 0 || T <= 0) {
+      set_error("spk_model_forward: invalid argument");
+      return SPK_E_INVALID;
+    }
+    int dev = 0;
+    if (int rc = hip_check(hipGetDevice(&dev), "hipGetDevice")) return rc;
+    if (dev != model->m.device) {
+      set_error("spk_model_forward: handle belongs to another device");
+      return SPK_E_DEVICE;
+    }
+    Plan* plan = get_plan(model, B, T);
+    if (workspace_bytes < plan->ws_bytes || (plan->ws_bytes && !workspace)) {
+      set_error("spk_model_forward: workspace too small (need " + std::to_string(plan->ws_bytes) + " bytes)");
+      return SPK_E_WORKSPACE;
+    }
+    Ctx c{reinterpret_cast<char*>(workspace), feats, emb_out, reinterpret_cast<hipStream_t>(stream)};
+    for (size_t i = 0; i < plan->steps.size(); ++i) {
+      hipError_t e = plan->steps[i](c);
+      if (e != hipSuccess) {
+        set_error("spk_model_forward: step '" + plan->names[i] + "': " + hipGetErrorString(e));
+        return SPK_E_HIP;
+      }
+    }
+    return SPK_OK;
+  });
+}
+
+int spk_model_plan_size(spk_model_t* model, int32_t B, int32_t T, int32_t* n_steps) {
+  return guarded([&]() -> int {
+    if (!model || !n_steps || B <= 0 || T <= 0) return SPK_E_INVALID;
+    *n_steps = (int32_t)get_plan(model, B, T)->steps.size();
+    return SPK_OK;
+  });
+}
+
+int spk_model_plan_step(spk_model_t* model, int32_t B, int32_t T, int32_t i, char* name, int32_t name_len,
+                        char* kernel, int32_t kernel_len, double* flops) {
+  return guarded([&]() -> int {
+    if (!model || B <= 0 || T <= 0) return SPK_E_INVALID;
+    Plan* p = get_plan(model, B, T);
+    if (i < 0 || i >= (int)p->steps.size()) return SPK_E_INVALID;
+    if (name && name_len > 0) { std::strncpy(name, p->names[i].c_str(), name_len - 1); name[name_len - 1] = 0; }
+    if (kernel && kernel_len > 0) {
+      std::strncpy(kernel, p->kernels[i].c_str(), kernel_len - 1);
+      kernel[kernel_len - 1] = 0;
+    }
+    if (flops) *flops = p->flops[i];
+    return SPK_OK;
+  });
+}
+
+int spk_model_forward_timed(spk_model_t* model, const float* feats, int32_t B, int32_t T, void* workspace,
+                            size_t workspace_bytes, float* emb_out, void* stream, float* step_ms, int32_t max_steps) {
+  return guarded([&]() -> int {
+    if (!model || !feats || !emb_out || !step_ms || B <= 0 || T <= 0) return SPK_E_INVALID;
+    Plan* plan = get_plan(model, B, T);
+    const int n = (int)plan->steps.size();
+    if (max_steps < n) { set_error("spk_model_forward_timed: step_ms too short"); return SPK_E_INVALID; }
+    if (workspace_bytes < plan->ws_bytes) return SPK_E_WORKSPACE;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    std::vector<hipEvent_t> ev(n + 1);
+    for (auto& e : ev)
+      if (int rc = hip_check(hipEventCreate(&e), "hipEventCreate")) return rc;
+    Ctx c{reinterpret_cast<char*>(workspace), feats, emb_out, s};
+    int rc = SPK_OK;
+    (void)hipEventRecord(ev[0], s);
+    for (int i = 0; i < n && rc == SPK_OK; ++i) {
+      hipError_t e = plan->steps[i](c);
+      if (e != hipSuccess) {
+        set_error("step '" + plan->names[i] + "': " + hipGetErrorString(e));
+        rc = SPK_E_HIP;
+      }
+      (void)hipEventRecord(ev[i + 1], s);
+    }
+    if (rc == SPK_OK) rc = hip_check(hipEventSynchronize(ev[n]), "hipEventSynchronize");
+    for (int i = 0; i < n && rc == SPK_OK; ++i) (void)hipEventElapsedTime(&step_ms[i], ev[i], ev[i + 1]);
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    return rc;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,136 @@
+// Native executor: weight folding/packing, per-shape launch plans, workspace layout.
+#pragma once
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/spk_hip.h"
+#include "common.h"
+
+namespace spk {
+
+struct SpkError : std::runtime_error {
+  int code;
+  SpkError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+// A pointer resolved at launch time: into the caller's workspace, the input features, the
+// output embeddings, or the model's packed weights (absolute).
+struct Buf {
+  enum Kind { NONE = 0, WS = 1, IN = 2, OUT = 3, ABS = 4 };
+  int kind = NONE;
+  size_t off = 0;           // bytes (WS/IN/OUT) ; ABS uses ptr
+  const float* ptr = nullptr;
+  Buf at(size_t floats) const { Buf b = *this; if (kind == ABS) b.ptr += floats; else b.off += floats * 4; return b; }
+  explicit operator bool() const { return kind != NONE; }
+};
+
+struct Ctx {
+  char* ws;
+  const float* in;
+  float* out;
+  hipStream_t stream;
+  float* resolve(const Buf& b) const {
+    switch (b.kind) {
+      case Buf::WS: return reinterpret_cast<float*>(ws + b.off);
+      case Buf::IN: return const_cast<float*>(reinterpret_cast<const float*>(reinterpret_cast<const char*>(in) + b.off));
+      case Buf::OUT: return reinterpret_cast<float*>(reinterpret_cast<char*>(out) + b.off);
+      case Buf::ABS: return const_cast<float*>(b.ptr);
+      default: return nullptr;
+    }
+  }
+};
+
+using Step = std::function<hipError_t(const Ctx&)>;
+
+struct Plan {
+  std::vector<Step> steps;
+  std::vector<std::string> names;   // for error messages / tracing
+  std::vector<std::string> kernels; // kernel instantiation each step launches
+  std::vector<double> flops;        // algorithmic FLOPs of the step (whole batch)
+  size_t ws_bytes = 0;
+};
+
+// Logical -> physical channel map of a channels-last tensor (zero-padded slices).
+struct ChanMap {
+  std::vector<int> phys;
+  int n_phys = 0;
+  static ChanMap dense(int c, int align = 4);
+  static ChanMap slices(int width, int n, int align = 4);   // n slices of `width`, each padded
+  int n_log() const { return (int)phys.size(); }
+};
+
+// Packed GEMM operand: weights [N][Kp] (+ bias [N]) at offsets of the model's arena.
+struct Packed {
+  size_t w_off = 0, b_off = 0;
+  int N = 0, K = 0, Kp = 0;
+  size_t ps_off = SIZE_MAX, pt_off = SIZE_MAX;   // optional post-activation affine
+  bool has_bias = false;
+};
+
+// One weight tensor's contribution to a packed GEMM.
+struct Part {
+  std::string wkey;        // conv / linear weight [Cout][Cin](...[kh][kw])
+  std::string bias_key;    // optional conv bias
+  std::string bn;          // optional BatchNorm prefix folded into this part
+  ChanMap in;              // physical layout of the part's input source
+  int ci_lo = 0;           // first logical input channel of the weight read by this part
+  int kofs = 0;            // K offset of this part in the packed matrix
+};
+
+struct Model {
+  spk_model_config_t cfg{};
+  int device = 0;
+  struct HostT { std::vector<int64_t> shape; std::vector<float> data; };
+  std::map<std::string, HostT> W;                 // host copies (dropped after create)
+  std::vector<float> arena;                       // packed host weights (dropped after upload)
+  float* dweights = nullptr;
+  size_t dweights_bytes = 0;
+  std::map<std::string, Packed> packed;
+  std::map<std::pair<int, int>, std::unique_ptr<Plan>> plans;
+  std::mutex mu;
+  bool uploaded = false;
+
+  std::map<std::string, std::vector<int64_t>> shapes;   // every state_dict key (kept for the handle's life)
+
+  const HostT& get(const std::string& k) const;
+  bool has(const std::string& k) const { return shapes.count(k) != 0; }
+  int64_t dim(const std::string& k, int i) const;
+
+  size_t put(const std::vector<float>& v);        // append 64-float aligned, return offset (floats)
+  const float* dptr(size_t off) const { return dweights + off; }
+  // fold BN (+conv bias) into per-output-channel (scale, shift) in double precision
+  void bn_fold(const std::string& bn, int n, std::vector<double>& s, std::vector<double>& t, double eps = 1e-5) const;
+  const Packed& pack(const std::string& name, const ChanMap& out, const std::vector<Part>& parts, int K);
+  const Packed& pack_post_affine(const std::string& name, const std::string& bn, const ChanMap& out);
+};
+
+// Per-architecture graph builders.  With plan == nullptr they only pack weights.
+struct Builder {
+  Model& m;
+  Plan* plan;
+  int B;
+  size_t ws = 0;
+  double macs_per_utt = 0;   // algorithmic conv/linear MACs for this (T)
+  double macs_at_last_step = 0;
+  Builder(Model& mm, Plan* p, int b) : m(mm), plan(p), B(b) {}
+  Buf alloc(size_t floats);
+  void step(const std::string& name, Step s, const std::string& kernel = "");
+  // emit an implicit-GEMM conv; pointers of `d` are taken from the Bufs
+  struct ConvIO {
+    Buf s0, s0b, s1, out, res, affx, affy, gate, partial;
+  };
+  void conv(const std::string& name, ConvDesc d, const Packed& p, const ConvIO& io, bool use_bias = true);
+};
+
+void build_eres2net(Builder& b, int T, bool v2);
+void build_ecapa(Builder& b, int T);
+void build_campplus(Builder& b, int T);
+
+void set_error(const std::string& msg);
+
+}  // namespace spk

@@ -1,0 +1,295 @@
+"""ctypes binding of ``libspk_hip.so`` (declared in ``include/spk_hip.h``).
+
+This is the only bridge between the drop-in Python surface and the HIP kernels.  There is
+no CPU fallback: if the shared library is missing, or a tensor is not on a ROCm device,
+the call raises.  (The CPU restatement used to *check* results lives in ``oracle/`` and
+is imported by tests only.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Dict, Optional
+
+import torch
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # .../3d-speaker_amd
+LIB_PATH = os.environ.get('SPK_HIP_LIB', os.path.join(_PKG_ROOT, 'lib', 'libspk_hip.so'))
+
+ARCH_ERES2NETV2 = 1
+ARCH_ERES2NET = 2
+ARCH_ECAPA = 3
+ARCH_CAMPPLUS = 4
+
+
+class spk_weight_t(ctypes.Structure):
+    _fields_ = [('name', ctypes.c_char_p), ('data', ctypes.c_void_p), ('ndim', ctypes.c_int32),
+                ('shape', ctypes.c_int64 * 4)]
+
+
+class spk_model_config_t(ctypes.Structure):
+    _fields_ = [('arch', ctypes.c_int32), ('feat_dim', ctypes.c_int32), ('embed_dim', ctypes.c_int32),
+                ('m_channels', ctypes.c_int32), ('base_width', ctypes.c_int32), ('scale', ctypes.c_int32),
+                ('expansion', ctypes.c_int32), ('two_emb_layer', ctypes.c_int32),
+                ('channels', ctypes.c_int32 * 5), ('kernel_sizes', ctypes.c_int32 * 5),
+                ('dilations', ctypes.c_int32 * 5), ('reserved', ctypes.c_int32 * 8)]
+
+
+# every entry point of include/spk_hip.h: name -> (restype, argtypes)
+_P = ctypes.c_void_p
+SYMBOLS = {
+    'spk_version': (ctypes.c_int, []),
+    'spk_last_error': (ctypes.c_char_p, []),
+    'spk_fbank_f32': (ctypes.c_int, [_P, _P, ctypes.c_int32, _P, _P, ctypes.c_int32, ctypes.c_int32, _P]),
+    'spk_model_create': (ctypes.c_int, [ctypes.POINTER(spk_model_config_t), ctypes.POINTER(spk_weight_t),
+                                        ctypes.c_int32, ctypes.POINTER(_P)]),
+    'spk_model_destroy': (ctypes.c_int, [_P]),
+    'spk_model_workspace_bytes': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_size_t)]),
+    'spk_model_forward': (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_size_t, _P, _P]),
+    'spk_model_flops': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_double)]),
+    'spk_model_plan_size': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
+    'spk_model_plan_step': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p,
+                                           ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32,
+                                           ctypes.POINTER(ctypes.c_double)]),
+    'spk_model_forward_timed': (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_size_t, _P, _P,
+                                               _P, ctypes.c_int32]),
+    'spk_cosine_affinity': (ctypes.c_int, [_P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int32, _P,
+                                           ctypes.c_int64, _P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libspk_hip.so once (after torch, so it shares torch's HIP runtime)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise HipError(f'libspk_hip.so not found at {LIB_PATH}: build it with '
+                               f'`python -c "import __graft_entry__ as g; g.build()"` (or make -C 3d-speaker_amd/csrc)')
+            handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            for name, (res, args) in SYMBOLS.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = handle
+    return _lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().spk_last_error()
+        raise HipError(f'{what} failed ({rc}): {msg.decode() if msg else ""}')
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device_tensor(x: torch.Tensor, what: str):
+    if not isinstance(x, torch.Tensor) or x.device.type != 'cuda':
+        raise HipError(f'{what}: the MI355X path needs a ROCm device tensor (got '
+                       f'{getattr(x, "device", type(x))}); move the input with .to("cuda")')
+
+
+# ----------------------------------------------------------------------------- Fbank
+_frame_offsets_cache: Dict = {}
+
+
+def num_frames(n_samples: int) -> int:
+    return 0 if n_samples < 400 else 1 + (n_samples - 400) // 160
+
+
+def fbank(wavs: torch.Tensor, n_mels: int = 80, mean_nor: bool = False, lengths=None) -> torch.Tensor:
+    """Batched Kaldi Fbank on the GPU.
+
+    ``wavs``: [B, L] float32 device tensor (or [L]).  With ``lengths`` (list of ints) the
+    rows are ragged (samples beyond each length are ignored) and the result is a list of
+    [T_i, n_mels] views into one buffer; otherwise [B, T, n_mels].
+    """
+    require_device_tensor(wavs, 'fbank')
+    squeeze = wavs.dim() == 1
+    if squeeze:
+        wavs = wavs.unsqueeze(0)
+    wavs = wavs.to(torch.float32).contiguous()
+    B, L = wavs.shape
+    dev = wavs.device
+    if lengths is None:
+        lens = [L] * B
+    else:
+        lens = [int(v) for v in lengths]
+    frames = [num_frames(n) for n in lens]
+    frame_off = [0]
+    for f in frames:
+        frame_off.append(frame_off[-1] + f)
+    wav_off = [i * L for i in range(B + 1)]
+    offs = torch.tensor([wav_off, frame_off], dtype=torch.int64).to(dev, non_blocking=True)
+    feats = torch.empty((frame_off[-1], n_mels), dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _check(lib().spk_fbank_f32(wavs.data_ptr(), offs[0].data_ptr(), B, feats.data_ptr(), offs[1].data_ptr(),
+                                   n_mels, int(bool(mean_nor)), _stream(dev)), 'spk_fbank_f32')
+    if lengths is not None:
+        return [feats[frame_off[i]:frame_off[i + 1]] for i in range(B)]
+    out = feats.view(B, frames[0], n_mels)
+    return out[0] if squeeze else out
+
+
+# ----------------------------------------------------------------------------- models
+class NativeModel:
+    """One ``spk_model_t`` handle (folded + packed weights on one device)."""
+
+    def __init__(self, arch: int, cfg: dict, state_dict, device: torch.device):
+        c = spk_model_config_t()
+        c.arch = arch
+        for k in ('feat_dim', 'embed_dim', 'm_channels', 'base_width', 'scale', 'expansion', 'two_emb_layer'):
+            setattr(c, k, int(cfg.get(k, 0)))
+        for k in ('channels', 'kernel_sizes', 'dilations'):
+            vals = list(cfg.get(k, []))[:5]
+            getattr(c, k)[:len(vals)] = vals
+        self.embed_dim = int(cfg['embed_dim'])
+        self.device = device
+        host = []
+        ws = (spk_weight_t * len(state_dict))()
+        for i, (name, t) in enumerate(state_dict.items()):
+            ws[i].name = name.encode()
+            ws[i].ndim = t.dim()
+            for d in range(min(t.dim(), 4)):
+                ws[i].shape[d] = t.shape[d]
+            if t.is_floating_point():
+                h = t.detach().to('cpu', torch.float32).contiguous()
+                host.append(h)
+                ws[i].data = h.data_ptr()
+            else:
+                ws[i].data = None
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            _check(lib().spk_model_create(ctypes.byref(c), ws, len(state_dict), ctypes.byref(handle)),
+                   'spk_model_create')
+        self.handle = handle
+        self._ws: Optional[torch.Tensor] = None
+
+    def __del__(self):
+        h = getattr(self, 'handle', None)
+        if h is not None and _lib is not None:
+            try:
+                _lib.spk_model_destroy(h)
+            except Exception:
+                pass
+
+    def workspace_bytes(self, B: int, T: int) -> int:
+        n = ctypes.c_size_t()
+        _check(lib().spk_model_workspace_bytes(self.handle, B, T, ctypes.byref(n)), 'spk_model_workspace_bytes')
+        return n.value
+
+    def flops(self, T: int) -> float:
+        f = ctypes.c_double()
+        _check(lib().spk_model_flops(self.handle, T, ctypes.byref(f)), 'spk_model_flops')
+        return f.value
+
+    def plan(self, B: int, T: int):
+        """[(step name, kernel name, algorithmic FLOPs)] of the launch plan for [B, T]."""
+        n = ctypes.c_int32()
+        _check(lib().spk_model_plan_size(self.handle, B, T, ctypes.byref(n)), 'spk_model_plan_size')
+        out = []
+        for i in range(n.value):
+            name = ctypes.create_string_buffer(256)
+            kern = ctypes.create_string_buffer(256)
+            fl = ctypes.c_double()
+            _check(lib().spk_model_plan_step(self.handle, B, T, i, name, 256, kern, 256, ctypes.byref(fl)),
+                   'spk_model_plan_step')
+            out.append((name.value.decode(), kern.value.decode(), fl.value))
+        return out
+
+    def forward_timed(self, feats: torch.Tensor, out: torch.Tensor):
+        """forward() with a HIP event around every plan step; returns per-step ms."""
+        B, T, _ = feats.shape
+        n = len(self.plan(B, T))
+        ms = (ctypes.c_float * n)()
+        with torch.cuda.device(self.device):
+            need = self.workspace_bytes(B, T)
+            if self._ws is None or self._ws.numel() < need:
+                self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+            _check(lib().spk_model_forward_timed(self.handle, feats.data_ptr(), B, T, self._ws.data_ptr(),
+                                                 self._ws.numel(), out.data_ptr(), _stream(self.device), ms, n),
+                   'spk_model_forward_timed')
+        return list(ms)
+
+    def forward(self, feats: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        require_device_tensor(feats, 'embedding forward')
+        if feats.device != self.device:
+            raise HipError(f'model handle lives on {self.device}, input on {feats.device}')
+        if feats.dim() != 3:
+            raise HipError(f'expected feats [B, T, F], got {tuple(feats.shape)}')
+        feats = feats.to(torch.float32).contiguous()
+        B, T, _ = feats.shape
+        with torch.cuda.device(self.device):
+            need = self.workspace_bytes(B, T)
+            if self._ws is None or self._ws.numel() < need:
+                self._ws = None
+                self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+            if out is None:
+                out = torch.empty((B, self.embed_dim), dtype=torch.float32, device=self.device)
+            _check(lib().spk_model_forward(self.handle, feats.data_ptr(), B, T, self._ws.data_ptr(),
+                                           self._ws.numel(), out.data_ptr(), _stream(self.device)),
+                   'spk_model_forward')
+        return out
+
+
+class HipModuleMixin:
+    """Mixin for the drop-in nn.Modules: lazily builds one native handle per device from
+    the module's own state_dict and drops it whenever weights are reloaded or moved."""
+
+    _hip_arch: int = 0
+
+    def _hip_config(self) -> dict:  # pragma: no cover - overridden
+        raise NotImplementedError
+
+    def _hip_reset(self, *args, **kwargs):
+        self.__dict__['_hip_handles'] = {}
+
+    def _hip_handle(self, device: torch.device) -> NativeModel:
+        handles = self.__dict__.setdefault('_hip_handles', {})
+        key = (device.type, device.index)
+        h = handles.get(key)
+        if h is None:
+            h = NativeModel(self._hip_arch, self._hip_config(), self.state_dict(), device)
+            handles[key] = h
+        return h
+
+    def _hip_forward(self, x: torch.Tensor) -> torch.Tensor:
+        require_device_tensor(x, type(self).__name__ + '.forward')
+        if self.training:
+            raise HipError(f'{type(self).__name__}: the MI355X path is inference-only; call .eval()')
+        dev = x.device if x.device.index is not None else torch.device('cuda', torch.cuda.current_device())
+        return self._hip_handle(dev).forward(x)
+
+    def _apply(self, fn, *args, **kwargs):
+        self._hip_reset()
+        return super()._apply(fn, *args, **kwargs)
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self._hip_reset()
+        return super()._load_from_state_dict(*args, **kwargs)
+
+
+def cosine_affinity(a: torch.Tensor, b: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None):
+    """[Na, E] x [Nb, E] -> [Na, Nb] cosine similarity on the GPU (sklearn semantics)."""
+    require_device_tensor(a, 'cosine_affinity')
+    b = a if b is None else b
+    a = a.to(torch.float32).contiguous()
+    b = b.to(torch.float32).contiguous()
+    if out is None:
+        out = torch.empty((a.shape[0], b.shape[0]), dtype=torch.float32, device=a.device)
+    with torch.cuda.device(a.device):
+        _check(lib().spk_cosine_affinity(a.data_ptr(), a.shape[0], b.data_ptr(), b.shape[0], a.shape[1],
+                                         out.data_ptr(), out.stride(0), _stream(a.device)), 'spk_cosine_affinity')
+    return out

@@ -1,0 +1,215 @@
+"""Headline benchmark: utterance-embeddings/sec (2 s @ 16 kHz), ERes2NetV2, fp32.
+
+BASELINE.json configs[1]: ERes2NetV2 (17.8 M) batch=256 2 s segments, 1x MI355X fp32.
+One step = the hot path over one batch of synthetic audio already resident in HBM:
+GPU Kaldi Fbank (80 mel, mean-normalised) of 256 x 32000 samples -> ERes2NetV2 forward
+-> 256 x 192 embeddings.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Multi-GPU: utterances shard with no data-path collective (weak scaling: every rank embeds
+its own 256-utterance batches); the barrier + max-over-ranks timing is the only
+communication.  Rank 0 prints ONE JSON line.  The roofline object describes the dominant
+kernel (largest total time inside one forward), measured with HIP events on the stream
+the kernels run on; the CPU baseline is the oracle (op-for-op torch CPU restatement)
+timed on this host on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, '3d-speaker_amd')):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 matrix (MFMA) peak
+PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E spec peak
+BATCH = 256
+SAMPLES = 32000               # 2 s @ 16 kHz -> 198 frames
+METRIC = 'utterance-embeddings/sec (2 s @16 kHz)'
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--batch', type=int, default=BATCH)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-seconds', type=float, default=12.0)
+    ap.add_argument('--traffic-json', default=os.path.join(REPO, 'profiles', 'pmc_traffic.json'),
+                    help='per-launch HBM bytes of the dominant kernel from a rocprofv3 --pmc pass (optional)')
+    return ap.parse_args()
+
+
+def build_model(device):
+    from speakerlab.models.eres2net.ERes2NetV2 import ERes2NetV2
+    from speakerlab.utils import synthetic
+    bn_path = os.path.join(REPO, 'tests', 'golden', 'eres2netv2_bn.npz')
+    bn = dict(np.load(bn_path)) if os.path.exists(bn_path) else None
+    model = ERes2NetV2(feat_dim=80, embedding_size=192)
+    synthetic.load_synthetic_weights(model, seed=0, bn_stats=bn)
+    return model.eval().to(device)
+
+
+def roofline(model, feats, device, traffic_json):
+    """Per-step HIP-event timing of one forward; dominant kernel = largest total time."""
+    h = model._hip_handle(device)
+    B, T, _ = feats.shape
+    plan = h.plan(B, T)
+    out = torch.empty(B, 192, device=device)
+    times = None
+    for _ in range(3):                        # keep the last of 3 (warm)
+        times = h.forward_timed(feats, out)
+    groups = {}
+    for (name, kern, fl), ms in zip(plan, times):
+        g = groups.setdefault(kern, {'ms': 0.0, 'flops': 0.0, 'launches': 0})
+        g['ms'] += ms
+        g['flops'] += fl
+        g['launches'] += 1
+    kern, g = max(groups.items(), key=lambda kv: kv[1]['ms'])
+    avg_ms = g['ms'] / g['launches']
+    flops_per_launch = g['flops'] / g['launches']
+    achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
+    conv_ms = sum(v['ms'] for k, v in groups.items() if k.startswith('conv_gemm'))
+    conv_fl = sum(v['flops'] for k, v in groups.items() if k.startswith('conv_gemm'))
+    traffic = None
+    if traffic_json and os.path.exists(traffic_json):
+        try:
+            traffic = json.load(open(traffic_json)).get(kern)
+        except Exception:
+            traffic = None
+    return {
+        'kernel': kern,
+        'bound': 'mfma',
+        'achieved': round(achieved, 3),
+        'peak': PEAK_FP32_TFLOPS,
+        'unit': 'TFLOP/s',
+        'frac': round(achieved / PEAK_FP32_TFLOPS, 4),
+        'traffic': traffic,
+        'launches_per_step': g['launches'],
+        'avg_launch_ms': round(avg_ms, 4),
+        'flops_per_launch': flops_per_launch,
+        'all_conv_gemm': {'achieved': round(conv_fl / (conv_ms * 1e-3) / 1e12, 3),
+                          'frac': round(conv_fl / (conv_ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
+                          'ms_per_forward': round(conv_ms, 3)},
+        'forward_ms_sum_of_steps': round(sum(times), 3),
+        'per_kernel_ms': {k: round(v['ms'], 3) for k, v in sorted(groups.items(), key=lambda kv: -kv[1]['ms'])},
+    }
+
+
+def cpu_baseline(seconds):
+    """Oracle (op-for-op torch CPU restatement + numpy Fbank), bounded sample."""
+    from oracle import fbank_ref, models_ref
+    from speakerlab.utils import synthetic
+    from speakerlab.models.eres2net.ERes2NetV2 import ERes2NetV2
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    bn = dict(np.load(os.path.join(REPO, 'tests', 'golden', 'eres2netv2_bn.npz')))
+    sd = synthetic.load_synthetic_weights(ERes2NetV2(feat_dim=80, embedding_size=192), 0, bn).state_dict()
+    wavs = synthetic.pcm16_batch(16, SAMPLES, seed=99)
+
+    def one():
+        feats = torch.from_numpy(fbank_ref.fbank_batch(wavs, 80, mean_nor=True))
+        return models_ref.forward('eres2netv2', sd, feats)
+
+    one()   # warm-up
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        one()
+        n += wavs.shape[0]
+    dt = time.perf_counter() - t0
+    return {'value': round(n / dt, 3), 'unit': 'utt/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{n} utterances of 2 s (batches of 16), numpy Fbank + torch CPU fp32 oracle forward, '
+                      f'{dt:.1f} s wall'}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        tdist.init_process_group('nccl' if torch.cuda.is_available() else 'gloo')
+    device = torch.device('cuda', local)
+    torch.cuda.set_device(device)
+
+    from speakerlab import _hip
+    from speakerlab.utils import synthetic
+
+    model = build_model(device)
+    B = args.batch
+    wavs = torch.from_numpy(synthetic.pcm16_batch(B, SAMPLES, seed=1 + 1000 * rank)).to(device)
+
+    def step():
+        feats = _hip.fbank(wavs, 80, mean_nor=True)
+        return model(feats)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if dist:
+            tdist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            emb = step()
+        torch.cuda.synchronize()
+        if dist:
+            tdist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        assert torch.isfinite(emb).all(), 'non-finite embeddings'
+        if dist:
+            t = torch.tensor([dt], device=device)
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+            dt = float(t.item())
+        feats = _hip.fbank(wavs, 80, mean_nor=True)
+        roof = roofline(model, feats, device, args.traffic_json) if rank == 0 else None
+
+    total_utts = B * args.steps * world
+    value = total_utts / dt
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(args.cpu_seconds)
+        flops = model._hip_handle(device).flops(198)
+        line = {
+            'metric': METRIC,
+            'value': round(value, 2),
+            'unit': 'utt/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': round(dt / args.steps * 1e3, 3),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'f32',
+            'data': 'synthetic PCM16 speech-like audio (numpy PCG64), deterministic synthetic weights',
+            'config': {'workload': 'ERes2NetV2 (17.8 M) batch=256 2 s segments, GPU Fbank + embedding, fp32',
+                       'model': 'ERes2NetV2', 'global_batch': B * world, 'seq_len': 198,
+                       'parallelism': f'dp{world} (utterance sharding, no collective)'},
+            'model_tflops_achieved': round(value * flops / 1e12, 3),
+            'model_gflop_per_utt': round(flops / 1e9, 3),
+            'roofline': roof,
+            'cpu_baseline': cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

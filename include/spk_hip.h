@@ -1,0 +1,124 @@
+/*
+ * spk_hip.h — C ABI of libspk_hip.so, the MI355X (gfx950) speaker-embedding hot path.
+ *
+ * Plain C, POD arguments only: device pointers are raw `float*`/`int64_t*` (owned by the
+ * caller, e.g. the torch caching allocator), streams are `hipStream_t` passed as `void*`.
+ * Every entry point returns 0 on success or a negative SPK_E_* code; the message of the
+ * last failure on the calling thread is available from spk_last_error().  No C++
+ * exception crosses this boundary.  Handles are immutable after creation, so one handle
+ * may be used from several streams concurrently; forward() allocates nothing (the caller
+ * provides a workspace sized by spk_model_workspace_bytes()), so it can be captured into
+ * a hipGraph.
+ *
+ * Which reference interface each entry point replaces (paths relative to the reference
+ * repo nanless/3D-Speaker):
+ *   spk_fbank_f32        speakerlab/process/processor.py:133-158 (FBank.__call__ ->
+ *                        torchaudio.compliance.kaldi.fbank) and the C++ runtime's
+ *                        FbankComputer::compute_feature runtime/onnxruntime/feature/feature_fbank.cpp:22-91
+ *   spk_model_create     model construction + strict load_state_dict in
+ *                        speakerlab/bin/infer_sv_batch.py:247-253 (and the ONNX session
+ *                        runtime/onnxruntime/model/speaker_embedding_model.cpp:7-40)
+ *   spk_model_forward    nn.Module.forward of ERes2NetV2.py:235-254, ERes2Net.py:208-231,
+ *                        ECAPA_TDNN.py:430-463, DTDNN.py:111-115 (and
+ *                        OnnxSpeakerEmbeddingModel::extract_embedding speaker_embedding_model.cpp:42-69)
+ *   spk_cosine_affinity  sklearn cosine_similarity as used by speakerlab/process/cluster.py:59-62,150
+ *                        and speakerlab/bin/compute_score_metrics.py:110-114
+ */
+#ifndef SPK_HIP_H
+#define SPK_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPK_OK 0
+#define SPK_E_INVALID (-1)     /* bad argument / shape */
+#define SPK_E_HIP (-2)         /* HIP runtime error */
+#define SPK_E_WEIGHTS (-3)     /* missing or mis-shaped state_dict tensor */
+#define SPK_E_DEVICE (-4)      /* handle used on another device */
+#define SPK_E_WORKSPACE (-5)   /* workspace too small */
+#define SPK_E_UNSUPPORTED (-6)
+
+/* architectures (the four models on the north-star path) */
+#define SPK_ARCH_ERES2NETV2 1  /* speakerlab.models.eres2net.ERes2NetV2.ERes2NetV2 */
+#define SPK_ARCH_ERES2NET 2    /* speakerlab.models.eres2net.ERes2Net.ERes2Net     */
+#define SPK_ARCH_ECAPA 3       /* speakerlab.models.ecapa_tdnn.ECAPA_TDNN.ECAPA_TDNN */
+#define SPK_ARCH_CAMPPLUS 4    /* speakerlab.models.campplus.DTDNN.CAMPPlus         */
+
+typedef struct spk_model spk_model_t;
+
+/* One state_dict tensor, HOST memory, float32 contiguous (int tensors such as
+ * num_batches_tracked may be passed with data == NULL).  Keys are the reference's. */
+typedef struct {
+  const char* name;
+  const float* data;
+  int32_t ndim;
+  int64_t shape[4];
+} spk_weight_t;
+
+/* Constructor arguments of the reference module (only those that shape the graph). */
+typedef struct {
+  int32_t arch;
+  int32_t feat_dim;       /* 80 */
+  int32_t embed_dim;      /* embedding_size / lin_neurons */
+  int32_t m_channels;     /* ERes2Net*: m_channels */
+  int32_t base_width;     /* ERes2NetV2: baseWidth (26); ERes2Net: 32 */
+  int32_t scale;          /* ERes2Net*: scale (2) */
+  int32_t expansion;      /* ERes2Net*: expansion (2) */
+  int32_t two_emb_layer;  /* ERes2Net*: two_emb_layer */
+  int32_t channels[5];    /* ECAPA: channels */
+  int32_t kernel_sizes[5];/* ECAPA: kernel_sizes */
+  int32_t dilations[5];   /* ECAPA: dilations */
+  int32_t reserved[8];
+} spk_model_config_t;
+
+int spk_version(void);
+const char* spk_last_error(void);
+
+/* Kaldi log-mel Fbank of a ragged batch.  wav: device float32 samples of all utterances
+ * back to back; wav_offsets/frame_offsets: DEVICE int64 arrays of n_utt+1 entries (sample
+ * and frame starts; frames = 1 + (len-400)/160).  feats: device [total_frames, n_mels]. */
+int spk_fbank_f32(const float* wav, const int64_t* wav_offsets, int32_t n_utt, float* feats,
+                  const int64_t* frame_offsets, int32_t n_mels, int32_t mean_nor, void* stream);
+
+/* Build a handle on the CURRENT HIP device: folds BatchNorm into conv weights, packs them
+ * for the kernels and uploads them (synchronous, once per model). */
+int spk_model_create(const spk_model_config_t* cfg, const spk_weight_t* weights, int32_t n_weights,
+                     spk_model_t** out);
+int spk_model_destroy(spk_model_t* model);
+
+/* Workspace bytes needed by spk_model_forward for a [B, T, feat_dim] batch. */
+int spk_model_workspace_bytes(spk_model_t* model, int32_t B, int32_t T, size_t* bytes);
+
+/* feats: device [B, T, feat_dim] float32; emb_out: device [B, embed_dim] float32. */
+int spk_model_forward(spk_model_t* model, const float* feats, int32_t B, int32_t T, void* workspace,
+                      size_t workspace_bytes, float* emb_out, void* stream);
+
+/* Algorithmic FLOPs per utterance of T frames (2 x conv/linear MACs). */
+int spk_model_flops(spk_model_t* model, int32_t T, double* flops);
+
+/* Introspection / measurement of the launch plan for a [B, T] batch: number of steps,
+ * each step's name, the kernel it launches (rocprofv3 naming) and its algorithmic FLOPs;
+ * spk_model_forward_timed() is spk_model_forward() with a HIP event around every step
+ * (synchronises; used by bench.py for the roofline figure, not for throughput). */
+int spk_model_plan_size(spk_model_t* model, int32_t B, int32_t T, int32_t* n_steps);
+int spk_model_plan_step(spk_model_t* model, int32_t B, int32_t T, int32_t i, char* name, int32_t name_len,
+                        char* kernel, int32_t kernel_len, double* flops);
+int spk_model_forward_timed(spk_model_t* model, const float* feats, int32_t B, int32_t T, void* workspace,
+                            size_t workspace_bytes, float* emb_out, void* stream, float* step_ms,
+                            int32_t max_steps);
+
+/* out[i*ldo + j] = <Ea_i, Eb_j> / (max(|Ea_i|,eps) * max(|Eb_j|,eps)), device pointers,
+ * row-major [Na,E] and [Nb,E] float32.  Matches sklearn cosine_similarity (normalize with
+ * zero-norm rows left as zero). */
+int spk_cosine_affinity(const float* Ea, int64_t Na, const float* Eb, int64_t Nb, int32_t E, float* out,
+                        int64_t ldo, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SPK_HIP_H */

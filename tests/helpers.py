@@ -1,0 +1,56 @@
+"""Shared test helpers: build the four models (product modules) with the deterministic
+synthetic weights + committed BN calibration fixtures, and load golden vectors."""
+import json
+import os
+
+import numpy as np
+import torch
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+ARCHS = ['eres2netv2', 'eres2net_large', 'ecapa', 'campplus']
+
+
+def product_module(arch):
+    if arch == 'eres2netv2':
+        from speakerlab.models.eres2net.ERes2NetV2 import ERes2NetV2
+        return ERes2NetV2(feat_dim=80, embedding_size=192)
+    if arch == 'eres2net_large':
+        from speakerlab.models.eres2net.ERes2Net import ERes2Net
+        return ERes2Net(feat_dim=80, embedding_size=192, m_channels=64)
+    if arch == 'ecapa':
+        from speakerlab.models.ecapa_tdnn.ECAPA_TDNN import ECAPA_TDNN
+        return ECAPA_TDNN(input_size=80, lin_neurons=192, channels=[1024, 1024, 1024, 1024, 3072])
+    if arch == 'campplus':
+        from speakerlab.models.campplus.DTDNN import CAMPPlus
+        return CAMPPlus(feat_dim=80, embedding_size=512)
+    raise KeyError(arch)
+
+
+def bn_stats(arch):
+    return dict(np.load(os.path.join(GOLDEN, f'{arch}_bn.npz')))
+
+
+def golden(arch):
+    return dict(np.load(os.path.join(GOLDEN, f'{arch}_golden.npz')))
+
+
+def ref_keys(arch):
+    with open(os.path.join(GOLDEN, f'{arch}_keys.json')) as f:
+        return json.load(f)
+
+
+def loaded_module(arch):
+    from speakerlab.utils import synthetic
+    m = product_module(arch)
+    synthetic.load_synthetic_weights(m, seed=0, bn_stats=bn_stats(arch))
+    return m.eval()
+
+
+def state_dict(arch, dtype=torch.float32):
+    return {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in loaded_module(arch).state_dict().items()}
+
+
+def rel_err(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return np.linalg.norm(a - b, axis=-1) / np.linalg.norm(b, axis=-1)

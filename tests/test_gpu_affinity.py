@@ -1,0 +1,26 @@
+"""GPU cosine affinity vs numpy (sklearn cosine_similarity semantics)."""
+import numpy as np
+import pytest
+import torch
+
+from speakerlab import _hip
+
+pytestmark = pytest.mark.gpu
+
+
+def ref_cos(a, b):
+    def norm(x):
+        n = np.linalg.norm(x, axis=1, keepdims=True)
+        n[n == 0] = 1.0
+        return x / n
+    return norm(a.astype(np.float64)) @ norm(b.astype(np.float64)).T
+
+
+@pytest.mark.parametrize('na,nb,e', [(1, 1, 192), (7, 300, 192), (257, 129, 512), (1000, 1000, 192)])
+def test_cosine_affinity(na, nb, e):
+    rng = np.random.default_rng(na + nb)
+    a = rng.standard_normal((na, e)).astype(np.float32)
+    b = rng.standard_normal((nb, e)).astype(np.float32)
+    a[0] = 0.0   # zero row -> zeros, like sklearn
+    out = _hip.cosine_affinity(torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()).cpu().numpy()
+    np.testing.assert_allclose(out, ref_cos(a, b), atol=2e-6)

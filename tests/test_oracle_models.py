@@ -1,0 +1,26 @@
+"""Pin the CPU oracle (oracle/models_ref.py) against golden embeddings produced by the
+reference modules themselves (tests/golden/make_golden.py)."""
+import numpy as np
+import pytest
+import torch
+
+import helpers
+from oracle import models_ref
+
+
+@pytest.mark.parametrize('arch', helpers.ARCHS)
+def test_oracle_matches_reference_fp32(arch):
+    g = helpers.golden(arch)
+    sd = helpers.state_dict(arch)
+    for i in range(3):
+        emb = models_ref.forward(arch, sd, torch.from_numpy(g[f'feats{i}'])).numpy()
+        # same op sequence in fp32: only summation-order noise
+        assert helpers.rel_err(emb, g[f'emb32_{i}']).max() < 2e-6, (arch, i)
+
+
+@pytest.mark.parametrize('arch', ['eres2netv2', 'campplus'])
+def test_oracle_matches_reference_fp64(arch):
+    g = helpers.golden(arch)
+    sd = helpers.state_dict(arch, torch.float64)
+    emb = models_ref.forward(arch, sd, torch.from_numpy(g['feats2']).double()).numpy()
+    assert helpers.rel_err(emb, g['emb64_2']).max() < 1e-12
