@@ -29,6 +29,11 @@ struct ConvSrc {
   int cin = 0;
   int kh = 1, kw = 1, sh = 1, sw = 1, ph = 0, pw = 0, dh = 1, dw = 1;
   int reflect = 0;             // speechbrain 'same' reflect padding (ECAPA Conv1d)
+  // optional pre-activation applied to in-bounds operand values: relu(v*scale[c] + shift[c])
+  // (CAM++ BN-ReLU in front of a conv; padding stays zero like the reference's F.pad of the
+  // activated tensor)
+  const float* pre_scale = nullptr;
+  const float* pre_shift = nullptr;
 };
 
 // out[m, n] = epi( sum_k A[m, k] * Wt[n, k] ), m = (img, ho, wo), k = (tap, c) of s0 then c of s1.
@@ -39,8 +44,10 @@ struct ConvDesc {
   int K = 0, Kp = 0;           // K = taps0*s0.cin + s1.cin ; Kp = round_up(K, 16)
   const float* w = nullptr;    // [N][Kp]
   const float* bias = nullptr; // [N] or null
+  const float* rowbias = nullptr; int rowbias_ld = 0;  // per-image bias [nimg][rowbias_ld] (ECAPA ASP context)
   float* out = nullptr; int ldo = 0;
   int act = ACT_NONE;
+  int act2 = ACT_NONE;         // applied after the post-affine (ECAPA ASP: BN then tanh)
   const float* res = nullptr; int ldr = 0;             // added before act
   const float* post_scale = nullptr;                   // after act: y*scale+shift (ECAPA BN after ReLU)
   const float* post_shift = nullptr;

@@ -117,6 +117,12 @@ conv_gemm_kernel(const ConvDesc d) {
     const int k = kt * BK + kq * 4;
     // ---- A
     if (k_ky < d.s0.kh) {
+      const bool pre = d.s0.pre_scale != nullptr;
+      f32x4 psc = {1.f, 1.f, 1.f, 1.f}, psh = {0.f, 0.f, 0.f, 0.f};
+      if (pre) {
+        psc = *reinterpret_cast<const f32x4*>(d.s0.pre_scale + k_c);
+        psh = *reinterpret_cast<const f32x4*>(d.s0.pre_shift + k_c);
+      }
 #pragma unroll
       for (int r = 0; r < AROWS; ++r) {
         int hi = a_hb[r] + k_ky * d.s0.dh;
@@ -131,6 +137,10 @@ conv_gemm_kernel(const ConvDesc d) {
           const size_t pix = (size_t)(a_img[r] * d.s0.H + hi) * d.s0.W + wi;
           v = *reinterpret_cast<const f32x4*>(d.s0.p + pix * d.s0.ld + k_c);
           if (ADD) v += *reinterpret_cast<const f32x4*>(d.s0.p2 + pix * d.s0.ld2 + k_c);
+          if (pre) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = fmaxf(fmaf(v[q], psc[q], psh[q]), 0.f);
+          }
         }
         ra[r] = v;
       }
@@ -258,6 +268,7 @@ conv_gemm_kernel(const ConvDesc d) {
         const int m = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         if (m >= M) continue;
         float v = acc[i][j][r] + bias;
+        if (d.rowbias) v += d.rowbias[(size_t)(m / (d.Ho * d.Wo)) * d.rowbias_ld + n];
         if (d.res) v += d.res[(size_t)m * d.ldr + n];
         if (d.affx) {
           const float t = 1.0f + tanhf(v);
@@ -265,6 +276,7 @@ conv_gemm_kernel(const ConvDesc d) {
         } else {
           v = apply_act(v, d.act);
           if (d.post_scale) v = v * ps + pt;
+          v = apply_act(v, d.act2);
         }
         if (d.gate) {
           const int wo = m % d.Wo;
@@ -284,9 +296,11 @@ __global__ void splitk_reduce_kernel(const ConvDesc d, int M) {
     float v = 0.f;
     for (int z = 0; z < d.ksplit; ++z) v += d.partial[(size_t)z * total + e];
     v += d.bias ? d.bias[n] : 0.f;
+    if (d.rowbias) v += d.rowbias[(size_t)(m / (d.Ho * d.Wo)) * d.rowbias_ld + n];
     if (d.res) v += d.res[(size_t)m * d.ldr + n];
     v = apply_act(v, d.act);
     if (d.post_scale) v = v * d.post_scale[n] + d.post_shift[n];
+    v = apply_act(v, d.act2);
     d.out[(size_t)m * d.ldo + n] = v;
   }
 }

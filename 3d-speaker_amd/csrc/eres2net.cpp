@@ -65,7 +65,7 @@ struct ERes2Builder {
     const ChanMap mid = ChanMap::dense(inter);
     const Packed& a0 = m.pack(p + ".la0", mid,
                               {Part{p + ".local_att.0.weight", p + ".local_att.0.bias", p + ".local_att.1", xin, 0, 0},
-                               Part{p + ".local_att.0.weight", "", "", xin, C, cp}},
+                               Part{p + ".local_att.0.weight", p + ".local_att.0.bias", p + ".local_att.1", xin, C, cp}},
                               2 * cp);
     const Packed& a1 = m.pack(p + ".la3", xin,
                               {Part{p + ".local_att.3.weight", p + ".local_att.3.bias", p + ".local_att.4", mid, 0, 0}},

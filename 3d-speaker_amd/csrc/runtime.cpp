@@ -177,6 +177,7 @@ void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const C
     d.affy = c.resolve(cio.affy);
     d.gate = c.resolve(cio.gate);
     d.partial = c.resolve(cio.partial);
+    d.rowbias = c.resolve(cio.rowbias);
     return launch_conv(d, c.stream);
   }, conv_kernel_name(probe));
 }

@@ -122,7 +122,7 @@ struct Builder {
   void step(const std::string& name, Step s, const std::string& kernel = "");
   // emit an implicit-GEMM conv; pointers of `d` are taken from the Bufs
   struct ConvIO {
-    Buf s0, s0b, s1, out, res, affx, affy, gate, partial;
+    Buf s0, s0b, s1, out, res, affx, affy, gate, partial, rowbias;
   };
   void conv(const std::string& name, ConvDesc d, const Packed& p, const ConvIO& io, bool use_bias = true);
 };

@@ -1,0 +1,166 @@
+// TEST INFRASTRUCTURE ONLY — host emulation of libspk_hip's kernel *contracts*.
+//
+// Built by tests/emu/Makefile into tests/emu/libspk_emu.so together with the unmodified
+// executor sources (runtime.cpp, eres2net.cpp, ...), so the launch plans, weight folding
+// and packing, channel layouts and workspace aliasing of the real library can be checked
+// against the oracle on a machine without a GPU.  "Device" pointers are host pointers.
+// It is never loaded by the product package; the GPU tests exercise the real kernels.
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "../../3d-speaker_amd/csrc/common.h"
+#include "../../3d-speaker_amd/csrc/fbank.h"
+#include "../../3d-speaker_amd/csrc/misc.h"
+
+namespace spk {
+
+static float act_f(float v, int act) {
+  switch (act) {
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_HTANH: return std::fmin(std::fmax(v, 0.f), 20.f);
+    case ACT_SILU: return v / (1.f + std::exp(-v));
+    case ACT_SIGMOID: return 1.f / (1.f + std::exp(-v));
+    case ACT_TANH: return std::tanh(v);
+    default: return v;
+  }
+}
+
+static float epilogue(const ConvDesc& d, int m, int n, float v) {
+  if (d.bias) v += d.bias[n];
+  if (d.rowbias) v += d.rowbias[(size_t)(m / (d.Ho * d.Wo)) * d.rowbias_ld + n];
+  if (d.res) v += d.res[(size_t)m * d.ldr + n];
+  if (d.affx) {
+    const float t = 1.0f + std::tanh(v);
+    return d.affx[(size_t)m * d.ldx + n] * t + d.affy[(size_t)m * d.ldy + n] * (2.0f - t);
+  }
+  v = act_f(v, d.act);
+  if (d.post_scale) v = v * d.post_scale[n] + d.post_shift[n];
+  v = act_f(v, d.act2);
+  if (d.gate) {
+    const int wo = m % d.Wo, img = m / (d.Wo * d.Ho);
+    v *= d.gate[((size_t)img * d.gate_nseg + wo / d.gate_seg) * d.gate_ld + n];
+  }
+  return v;
+}
+
+hipError_t launch_conv(const ConvDesc& d, hipStream_t) {
+  if (d.s0.cin % 4 || d.s0.ld % 4 || d.Kp % 16 || d.ldo < d.N || d.K > d.Kp) return hipErrorInvalidValue;
+  const int M = d.nimg * d.Ho * d.Wo;
+  const int K0 = d.s0.kh * d.s0.kw * d.s0.cin;
+  std::vector<float> a(d.Kp);
+  for (int m = 0; m < M; ++m) {
+    const int wo = m % d.Wo, ho = (m / d.Wo) % d.Ho, img = m / (d.Wo * d.Ho);
+    for (int k = 0; k < d.Kp; ++k) {
+      float v = 0.f;
+      if (k < K0) {
+        const int tap = k / d.s0.cin, c = k % d.s0.cin;
+        const int ky = tap / d.s0.kw, kx = tap % d.s0.kw;
+        int hi = ho * d.s0.sh - d.s0.ph + ky * d.s0.dh;
+        int wi = wo * d.s0.sw - d.s0.pw + kx * d.s0.dw;
+        if (d.s0.reflect) {
+          hi = hi < 0 ? -hi : (hi >= d.s0.H ? 2 * d.s0.H - 2 - hi : hi);
+          wi = wi < 0 ? -wi : (wi >= d.s0.W ? 2 * d.s0.W - 2 - wi : wi);
+        }
+        if (hi >= 0 && hi < d.s0.H && wi >= 0 && wi < d.s0.W) {
+          const size_t pix = (size_t)(img * d.s0.H + hi) * d.s0.W + wi;
+          v = d.s0.p[pix * d.s0.ld + c];
+          if (d.s0.p2) v += d.s0.p2[pix * d.s0.ld2 + c];
+          if (d.s0.pre_scale) v = std::fmax(v * d.s0.pre_scale[c] + d.s0.pre_shift[c], 0.f);
+        }
+      } else if (d.s1.p && k - K0 < d.s1.cin) {
+        const int c = k - K0;
+        const size_t pix = (size_t)(img * d.s1.H + ho * d.s1.sh) * d.s1.W + wo * d.s1.sw;
+        v = d.s1.p[pix * d.s1.ld + c];
+      }
+      a[k] = v;
+    }
+    for (int n = 0; n < d.N; ++n) {
+      const float* w = d.w + (size_t)n * d.Kp;
+      double acc = 0.0;
+      for (int k = 0; k < d.Kp; ++k) acc += (double)a[k] * w[k];
+      d.out[(size_t)m * d.ldo + n] = epilogue(d, m, n, (float)acc);
+    }
+  }
+  return hipSuccess;
+}
+
+std::string conv_kernel_name(const ConvDesc&) { return "emu_conv"; }
+
+hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const float* w, const float* bias, int cout,
+                               int act, int wstride, float* out, int ldo, hipStream_t) {
+  for (int b = 0; b < B; ++b)
+    for (int f = 0; f < F; ++f)
+      for (int t = 0; t < T; ++t)
+        for (int c = 0; c < cout; ++c) {
+          double acc = 0.0;
+          for (int dy = 0; dy < 3; ++dy)
+            for (int dx = 0; dx < 3; ++dx) {
+              const int ff = f + dy - 1, tt = t + dx - 1;
+              if (ff >= 0 && ff < F && tt >= 0 && tt < T) acc += (double)feats[((size_t)b * T + tt) * F + ff] * w[c * wstride + dy * 3 + dx];
+            }
+          float v = (float)acc + bias[c];
+          out[(((size_t)b * F + f) * T + t) * ldo + c] = act == ACT_RELU ? std::fmax(v, 0.f) : v;
+        }
+  return hipSuccess;
+}
+
+hipError_t launch_tstp(const float* x, int B, int H, int W, int C, int ld, float eps, int unbiased, float* out,
+                       hipStream_t) {
+  for (int b = 0; b < B; ++b)
+    for (int h = 0; h < H; ++h)
+      for (int c = 0; c < C; ++c) {
+        double s = 0, q = 0;
+        for (int t = 0; t < W; ++t) s += x[((size_t)(b * H + h) * W + t) * ld + c];
+        const double mean = s / W;
+        for (int t = 0; t < W; ++t) {
+          const double dl = x[((size_t)(b * H + h) * W + t) * ld + c] - mean;
+          q += dl * dl;
+        }
+        const double var = q / (unbiased ? W - 1 : W);
+        out[(size_t)b * 2 * H * C + h * C + c] = (float)mean;
+        out[(size_t)b * 2 * H * C + H * C + h * C + c] = (float)std::sqrt(var + eps);
+      }
+  return hipSuccess;
+}
+
+hipError_t launch_fbank(const float*, const int64_t*, int, float*, const int64_t*, int, int, const FbankTables*,
+                        hipStream_t) {
+  return hipErrorNotSupported;
+}
+
+hipError_t launch_cosine_affinity(const float* A, long long Na, const float* B, long long Nb, int E, float* out,
+                                  long long ldo, hipStream_t) {
+  for (long long i = 0; i < Na; ++i)
+    for (long long j = 0; j < Nb; ++j) {
+      double d = 0, na = 0, nb = 0;
+      for (int e = 0; e < E; ++e) {
+        d += (double)A[i * E + e] * B[j * E + e];
+        na += (double)A[i * E + e] * A[i * E + e];
+        nb += (double)B[j * E + e] * B[j * E + e];
+      }
+      na = na == 0 ? 1 : std::sqrt(na);
+      nb = nb == 0 ? 1 : std::sqrt(nb);
+      out[i * ldo + j] = (float)(d / (na * nb));
+    }
+  return hipSuccess;
+}
+
+}  // namespace spk
+
+// ---- HIP runtime API stubs (host memory stands in for device memory)
+extern "C" {
+hipError_t hipMalloc(void** p, size_t n) { *p = std::malloc(n ? n : 1); return *p ? hipSuccess : hipErrorOutOfMemory; }
+hipError_t hipFree(void* p) { std::free(p); return hipSuccess; }
+hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind) { std::memcpy(d, s, n); return hipSuccess; }
+hipError_t hipGetDevice(int* d) { *d = 0; return hipSuccess; }
+hipError_t hipGetLastError(void) { return hipSuccess; }
+const char* hipGetErrorString(hipError_t e) { return e == hipSuccess ? "hipSuccess" : "emulated hip error"; }
+hipError_t hipEventCreate(hipEvent_t* e) { *e = nullptr; return hipSuccess; }
+hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }
+hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
+hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
+hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) { std::memset(p, v, n); return hipSuccess; }
+}

@@ -1,0 +1,86 @@
+"""TEST INFRASTRUCTURE: run the real executor (plan building, BN folding, weight packing,
+channel layouts, workspace aliasing) on the host through tests/emu/libspk_emu.so, whose
+kernels are plain-loop emulations of the launch contracts in csrc/common.h.  Lets the
+plan logic be checked against the oracle without a GPU; the kernels themselves are
+checked by the -m gpu tests."""
+import ctypes
+import os
+import subprocess
+
+import torch
+
+from speakerlab import _hip
+
+EMU_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'emu')
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        subprocess.run(['make', '-s', '-C', EMU_DIR], check=True)
+        h = ctypes.CDLL(os.path.join(EMU_DIR, 'libspk_emu.so'))
+        for name, (res, args) in _hip.SYMBOLS.items():
+            fn = getattr(h, name)
+            fn.restype, fn.argtypes = res, args
+        _lib = h
+    return _lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f'{what}: {lib().spk_last_error().decode()}')
+
+
+class EmuModel:
+    def __init__(self, module):
+        cfg = module._hip_config()
+        c = _hip.spk_model_config_t()
+        c.arch = module._hip_arch
+        for k in ('feat_dim', 'embed_dim', 'm_channels', 'base_width', 'scale', 'expansion', 'two_emb_layer'):
+            setattr(c, k, int(cfg.get(k, 0)))
+        for k in ('channels', 'kernel_sizes', 'dilations'):
+            vals = list(cfg.get(k, []))[:5]
+            getattr(c, k)[:len(vals)] = vals
+        sd = module.state_dict()
+        self.embed_dim = int(cfg['embed_dim'])
+        host = []
+        ws = (_hip.spk_weight_t * len(sd))()
+        for i, (name, t) in enumerate(sd.items()):
+            ws[i].name = name.encode()
+            ws[i].ndim = t.dim()
+            for d in range(t.dim()):
+                ws[i].shape[d] = t.shape[d]
+            if t.is_floating_point():
+                h = t.detach().float().contiguous()
+                host.append(h)
+                ws[i].data = h.data_ptr()
+        self.handle = ctypes.c_void_p()
+        _check(lib().spk_model_create(ctypes.byref(c), ws, len(sd), ctypes.byref(self.handle)), 'create')
+
+    def __call__(self, feats):
+        feats = feats.float().contiguous()
+        B, T, _ = feats.shape
+        n = ctypes.c_size_t()
+        _check(lib().spk_model_workspace_bytes(self.handle, B, T, ctypes.byref(n)), 'workspace')
+        ws = torch.zeros(max(n.value, 256), dtype=torch.uint8)
+        out = torch.empty(B, self.embed_dim)
+        _check(lib().spk_model_forward(self.handle, feats.data_ptr(), B, T, ws.data_ptr(), ws.numel(),
+                                       out.data_ptr(), None), 'forward')
+        return out
+
+    def plan(self, B, T):
+        n = ctypes.c_int32()
+        _check(lib().spk_model_plan_size(self.handle, B, T, ctypes.byref(n)), 'plan_size')
+        steps = []
+        for i in range(n.value):
+            name = ctypes.create_string_buffer(256)
+            fl = ctypes.c_double()
+            _check(lib().spk_model_plan_step(self.handle, B, T, i, name, 256, None, 0, ctypes.byref(fl)), 'step')
+            steps.append((name.value.decode(), fl.value))
+        return steps
+
+    def flops(self, T):
+        f = ctypes.c_double()
+        _check(lib().spk_model_flops(self.handle, T, ctypes.byref(f)), 'flops')
+        return f.value

@@ -1,0 +1,29 @@
+"""Executor plan logic on the host (tests/emu): the real C++ plan builder + weight packing
+with emulated kernels must reproduce the oracle.  Catches layout / folding / aliasing bugs
+without a GPU; the GPU tests then only have to validate the kernels."""
+import numpy as np
+import pytest
+import torch
+
+import helpers
+from emu_runner import EmuModel
+from oracle import models_ref
+
+EMU_ARCHS = ['eres2netv2', 'eres2net_large']
+
+
+@pytest.mark.parametrize('arch', EMU_ARCHS)
+def test_emulated_plan_matches_oracle(arch):
+    g = helpers.golden(arch)
+    m = helpers.loaded_module(arch)
+    feats = torch.from_numpy(g['feats2'][:1])          # 1 x 98 frames keeps the loops quick
+    ref = g['emb64_2'][:1]
+    emb = EmuModel(m)(feats).numpy()
+    assert helpers.rel_err(emb, ref).max() < 1e-4
+
+
+@pytest.mark.parametrize('arch,gflop', [('eres2netv2', 16.533), ('eres2net_large', 26.747)])
+def test_algorithmic_flops_match_survey(arch, gflop):
+    """FLOPs per 2 s utterance = 2 x conv/linear MACs (forward hooks)."""
+    fl = EmuModel(helpers.loaded_module(arch)).flops(198)
+    assert abs(fl / 1e9 - gflop) / gflop < 2e-3, fl
