@@ -60,6 +60,7 @@ struct ConvDesc {
 
 hipError_t launch_conv(const ConvDesc& d, hipStream_t s);
 std::string conv_kernel_name(const ConvDesc& d);
+int conv_tile_blocks(const ConvDesc& d);   // blocks of one split of the tile config launch_conv picks
 
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 

@@ -26,8 +26,7 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BK = 16;
-constexpr int LDS_ROW = BK + 4;   // floats per LDS row (pad: conflict-free ds_read_b128)
+constexpr int KP_ALIGN = 32;   // weights are packed with Kp a multiple of this
 
 __device__ __forceinline__ float apply_act(float v, int act) {
   switch (act) {
@@ -48,15 +47,47 @@ __device__ __forceinline__ int xcd_remap(int orig, int nblk) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
-template <int BM, int BN, int WM, int WN, bool S1, bool ADD>
-__global__ void __launch_bounds__(256)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One output element of the fused epilogue (everything after the K reduction).
+__device__ __forceinline__ float epilogue_elem(const ConvDesc& d, int m, int n, float v) {
+  if (d.bias) v += d.bias[n];
+  if (d.rowbias) v += d.rowbias[(size_t)(m / (d.Ho * d.Wo)) * d.rowbias_ld + n];
+  if (d.res) v += d.res[(size_t)m * d.ldr + n];
+  if (d.affx) {
+    const float t = 1.0f + tanhf(v);
+    return d.affx[(size_t)m * d.ldx + n] * t + d.affy[(size_t)m * d.ldy + n] * (2.0f - t);
+  }
+  v = apply_act(v, d.act);
+  if (d.post_scale) v = v * d.post_scale[n] + d.post_shift[n];
+  v = apply_act(v, d.act2);
+  if (d.gate) {
+    const int wo = m % d.Wo;
+    const int img = m / (d.Wo * d.Ho);
+    v *= d.gate[((size_t)img * d.gate_nseg + wo / d.gate_seg) * d.gate_ld + n];
+  }
+  return v;
+}
+
+template <int BM, int BN, int BK, int WM, int WN, bool S1, bool ADD>
+__global__ void __launch_bounds__(64 * WM * WN)
 conv_gemm_kernel(const ConvDesc d) {
-  constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int TM = WTM / 32, TN = WTN / 32;
-  constexpr int AROWS = BM / 64;                 // A rows staged per thread
-  constexpr int BROWS = (BN + 63) / 64;          // B rows staged per thread
-  static_assert(WM * WN == 4, "4 waves");
-  static_assert(TM >= 1 && TN >= 1, "wave tile >= 32x32");
+  constexpr int NT = 64 * WM * WN;               // threads
+  constexpr int WTM = BM / WM, WTN = BN / WN;    // wave tile
+  constexpr int TM = WTM / 32, TN = WTN / 32;    // 32x32 MFMA tiles per wave
+  constexpr int QPR = BK / 4;                    // float4 quads per tile row
+  constexpr int RPP = NT / QPR;                  // rows staged per pass
+  constexpr int AROWS = BM / RPP;                // A rows staged per thread
+  constexpr int BROWS = (BN + RPP - 1) / RPP;    // B rows staged per thread
+  constexpr int LDS_ROW = BK + 4;                // padded row: conflict-free ds_read_b128
+  constexpr int HK = BK / 2;                     // k values per lane half per tile
+  constexpr int FQ = HK / 4;                     // f32x4 per fragment
+  static_assert(TM >= 1 && TN >= 1 && BM % RPP == 0, "tile shape");
+  static_assert(2 * (BM + BN) * LDS_ROW >= WM * WN * 1024, "epilogue staging fits");
 
   __shared__ __attribute__((aligned(16))) float lds[2 * (BM + BN) * LDS_ROW];
   float* As = lds;                               // [2][BM][LDS_ROW]
@@ -79,12 +110,12 @@ conv_gemm_kernel(const ConvDesc d) {
   const int kt1 = min(nkt_all, kt0 + per);
 
   // ---- per-thread A-row geometry (fixed across the K loop)
-  const int kq = tid & 3;
+  const int kq = tid % QPR, row0 = tid / QPR;
   int a_img[AROWS], a_hb[AROWS], a_wb[AROWS], a_h1[AROWS], a_w1[AROWS];
   bool a_ok[AROWS];
 #pragma unroll
   for (int r = 0; r < AROWS; ++r) {
-    const int m = m0 + (tid >> 2) + 64 * r;
+    const int m = m0 + row0 + RPP * r;
     a_ok[r] = m < M;
     const int mm = a_ok[r] ? m : 0;
     const int wo = mm % d.Wo;
@@ -97,10 +128,10 @@ conv_gemm_kernel(const ConvDesc d) {
   }
   const int K0 = d.s0.kh * d.s0.kw * d.s0.cin;
 
-  // incremental (tap, channel) decomposition of this thread's k = kt*16 + kq*4
+  // incremental (tap, channel) decomposition of this thread's k = kt*BK + kq*4
   int k_c = 0, k_ky = 0, k_kx = 0;
   {
-    int k = kt0 * BK + kq * 4;
+    const int k = kt0 * BK + kq * 4;
     if (k < K0) {
       const int tap = k / d.s0.cin;
       k_c = k - tap * d.s0.cin;
@@ -115,7 +146,7 @@ conv_gemm_kernel(const ConvDesc d) {
 
   auto load_tile = [&](int kt) {
     const int k = kt * BK + kq * 4;
-    // ---- A
+    // ---- A (implicit im2col; zero outside the image / beyond K)
     if (k_ky < d.s0.kh) {
       const bool pre = d.s0.pre_scale != nullptr;
       f32x4 psc = {1.f, 1.f, 1.f, 1.f}, psh = {0.f, 0.f, 0.f, 0.f};
@@ -168,13 +199,12 @@ conv_gemm_kernel(const ConvDesc d) {
     } else {
       k_c += BK;
     }
-    // ---- B (weights [N][Kp])
+    // ---- B (packed weights [N][Kp])
 #pragma unroll
     for (int r = 0; r < BROWS; ++r) {
-      const int nr = (tid >> 2) + 64 * r;
+      const int nr = row0 + RPP * r;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (nr < BN && n0 + nr < d.N)
-        v = *reinterpret_cast<const f32x4*>(d.w + (size_t)(n0 + nr) * d.Kp + k);
+      if (nr < BN && n0 + nr < d.N) v = *reinterpret_cast<const f32x4*>(d.w + (size_t)(n0 + nr) * d.Kp + k);
       rb[r] = v;
     }
   };
@@ -183,11 +213,10 @@ conv_gemm_kernel(const ConvDesc d) {
     float* a = As + buf * BM * LDS_ROW;
     float* b = Bs + buf * BN * LDS_ROW;
 #pragma unroll
-    for (int r = 0; r < AROWS; ++r)
-      *reinterpret_cast<f32x4*>(a + ((tid >> 2) + 64 * r) * LDS_ROW + kq * 4) = ra[r];
+    for (int r = 0; r < AROWS; ++r) *reinterpret_cast<f32x4*>(a + (row0 + RPP * r) * LDS_ROW + kq * 4) = ra[r];
 #pragma unroll
     for (int r = 0; r < BROWS; ++r) {
-      const int nr = (tid >> 2) + 64 * r;
+      const int nr = row0 + RPP * r;
       if (nr < BN) *reinterpret_cast<f32x4*>(b + nr * LDS_ROW + kq * 4) = rb[r];
     }
   };
@@ -211,21 +240,22 @@ conv_gemm_kernel(const ConvDesc d) {
       if (kt + 1 < kt1) load_tile(kt + 1);
       const float* a = As + buf * BM * LDS_ROW;
       const float* b = Bs + buf * BN * LDS_ROW;
-      f32x4 af[TM][2], bf[TN][2];
+      // lane half lh owns k = lh*HK + s of this tile (same permutation for A and B)
+      f32x4 af[TM][FQ], bf[TN][FQ];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const float* p = a + (wm * WTM + i * 32 + li) * LDS_ROW + lh * 8;
-        af[i][0] = *reinterpret_cast<const f32x4*>(p);
-        af[i][1] = *reinterpret_cast<const f32x4*>(p + 4);
+        const float* p = a + (wm * WTM + i * 32 + li) * LDS_ROW + lh * HK;
+#pragma unroll
+        for (int q = 0; q < FQ; ++q) af[i][q] = *reinterpret_cast<const f32x4*>(p + 4 * q);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const float* p = b + (wn * WTN + j * 32 + li) * LDS_ROW + lh * 8;
-        bf[j][0] = *reinterpret_cast<const f32x4*>(p);
-        bf[j][1] = *reinterpret_cast<const f32x4*>(p + 4);
+        const float* p = b + (wn * WTN + j * 32 + li) * LDS_ROW + lh * HK;
+#pragma unroll
+        for (int q = 0; q < FQ; ++q) bf[j][q] = *reinterpret_cast<const f32x4*>(p + 4 * q);
       }
 #pragma unroll
-      for (int s = 0; s < 8; ++s)
+      for (int s = 0; s < HK; ++s)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -237,84 +267,70 @@ conv_gemm_kernel(const ConvDesc d) {
     }
   }
 
-  // ---- epilogue.  C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  if (d.ksplit > 1) {
-    float* part = d.partial + (size_t)blockIdx.z * M * d.N;
+  // ---- epilogue, one 32x32 accumulator tile at a time through a per-wave LDS slab:
+  // registers -> LDS in the MFMA C layout (col = lane&31, row = (r&3)+8(r>>2)+4(lane>>5)),
+  // then row-major sweeps (32 lanes = 128 contiguous output bytes) run the fused epilogue
+  // in a short loop instead of 16x-unrolled register code.
+  float* ct = lds + wave * 1024;
+  float* part = d.ksplit > 1 ? d.partial + (size_t)blockIdx.z * M * d.N : nullptr;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ct[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[i][j][r];
+      wave_lds_sync();
       const int n = n0 + wn * WTN + j * 32 + li;
-      if (n >= d.N) continue;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (m < M) part[(size_t)m * d.N + n] = acc[i][j][r];
+      const int mbase = m0 + wm * WTM + i * 32;
+#pragma unroll 2
+      for (int q = 0; q < 16; ++q) {
+        const int rl = 2 * q + lh;
+        const int m = mbase + rl;
+        if (m < M && n < d.N) {
+          const float v = ct[rl * 32 + li];
+          if (part) part[(size_t)m * d.N + n] = v;
+          else d.out[(size_t)m * d.ldo + n] = epilogue_elem(d, m, n, v);
         }
-    }
-    return;
-  }
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WTN + j * 32 + li;
-    if (n >= d.N) continue;
-    const float bias = d.bias ? d.bias[n] : 0.f;
-    const float ps = d.post_scale ? d.post_scale[n] : 1.f;
-    const float pt = d.post_shift ? d.post_shift[n] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (m >= M) continue;
-        float v = acc[i][j][r] + bias;
-        if (d.rowbias) v += d.rowbias[(size_t)(m / (d.Ho * d.Wo)) * d.rowbias_ld + n];
-        if (d.res) v += d.res[(size_t)m * d.ldr + n];
-        if (d.affx) {
-          const float t = 1.0f + tanhf(v);
-          v = d.affx[(size_t)m * d.ldx + n] * t + d.affy[(size_t)m * d.ldy + n] * (2.0f - t);
-        } else {
-          v = apply_act(v, d.act);
-          if (d.post_scale) v = v * ps + pt;
-          v = apply_act(v, d.act2);
-        }
-        if (d.gate) {
-          const int wo = m % d.Wo;
-          const int img = m / (d.Wo * d.Ho);
-          v *= d.gate[((size_t)img * d.gate_nseg + wo / d.gate_seg) * d.gate_ld + n];
-        }
-        d.out[(size_t)m * d.ldo + n] = v;
       }
-  }
+      wave_lds_sync();
+    }
 }
 
-// Split-K combine: out = epi(sum_z partial[z] + bias)   (fixed z order: deterministic)
+// Split-K combine: out = epi(sum_z partial[z])   (fixed z order: deterministic)
 __global__ void splitk_reduce_kernel(const ConvDesc d, int M) {
   const size_t total = (size_t)M * d.N;
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
     const int m = e / d.N, n = e % d.N;
     float v = 0.f;
     for (int z = 0; z < d.ksplit; ++z) v += d.partial[(size_t)z * total + e];
-    v += d.bias ? d.bias[n] : 0.f;
-    if (d.rowbias) v += d.rowbias[(size_t)(m / (d.Ho * d.Wo)) * d.rowbias_ld + n];
-    if (d.res) v += d.res[(size_t)m * d.ldr + n];
-    v = apply_act(v, d.act);
-    if (d.post_scale) v = v * d.post_scale[n] + d.post_shift[n];
-    v = apply_act(v, d.act2);
-    d.out[(size_t)m * d.ldo + n] = v;
+    d.out[(size_t)m * d.ldo + n] = epilogue_elem(d, m, n, v);
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+struct Cfg {
+  int bm, bn, bk, wm, wn;
+};
+
+Cfg select_cfg(const ConvDesc& d) {
+  const int M = d.nimg * d.Ho * d.Wo;
+  const int bk = d.Kp >= 256 ? 32 : 16;
+  if (d.N <= 32) return {256, 32, bk, 8, 1};
+  if (d.N <= 64) return {256, 64, bk, 4, 2};
+  if (M <= 4096) return {64, 128, bk, 1, 4};
+  return {128, 128, bk, 2, 4};
+}
+
+template <int BM, int BN, int BK, int WM, int WN>
 hipError_t launch_cfg(const ConvDesc& d, hipStream_t s) {
   const int M = d.nimg * d.Ho * d.Wo;
   const int nblk = ((M + BM - 1) / BM) * ((d.N + BN - 1) / BN);
   dim3 grid(nblk, 1, d.ksplit);
+  dim3 block(64 * WM * WN);
   const bool s1 = d.s1.p != nullptr, add = d.s0.p2 != nullptr;
   if (s1 && add) return hipErrorInvalidValue;
-  if (s1) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, true, false>), grid, dim3(256), 0, s, d);
-  else if (add) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, false, true>), grid, dim3(256), 0, s, d);
-  else hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, false, false>), grid, dim3(256), 0, s, d);
+  if (s1) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, true, false>), grid, block, 0, s, d);
+  else if (add) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, false, true>), grid, block, 0, s, d);
+  else hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, false, false>), grid, block, 0, s, d);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || d.ksplit <= 1) return e;
   const size_t total = (size_t)M * d.N;
@@ -323,34 +339,40 @@ hipError_t launch_cfg(const ConvDesc& d, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int BK>
+hipError_t launch_bk(const ConvDesc& d, const Cfg& c, hipStream_t s) {
+  if (c.bn == 32) return launch_cfg<256, 32, BK, 8, 1>(d, s);
+  if (c.bn == 64) return launch_cfg<256, 64, BK, 4, 2>(d, s);
+  if (c.bm == 64) return launch_cfg<64, 128, BK, 1, 4>(d, s);
+  return launch_cfg<128, 128, BK, 2, 4>(d, s);
+}
+
 }  // namespace
 
 // Name of the kernel instantiation launch_conv() picks (matches rocprofv3 kernel names).
 std::string conv_kernel_name(const ConvDesc& d) {
-  const int M = d.nimg * d.Ho * d.Wo;
-  int bm, bn, wm, wn;
-  if (d.N <= 32) { bm = 256; bn = 32; wm = 4; wn = 1; }
-  else if (d.N <= 64) { bm = 128; bn = 64; wm = 4; wn = 1; }
-  else if (M <= 4096) { bm = 64; bn = 128; wm = 1; wn = 4; }
-  else { bm = 128; bn = 128; wm = 2; wn = 2; }
+  const Cfg c = select_cfg(d);
   const bool s1 = d.s1.p != nullptr || d.s1.cin > 0, add = d.s0.p2 != nullptr || d.s0.ld2 > 0;
-  return "conv_gemm_kernel<" + std::to_string(bm) + ", " + std::to_string(bn) + ", " + std::to_string(wm) + ", " +
-         std::to_string(wn) + ", " + (s1 ? "true" : "false") + ", " + (add ? "true" : "false") + ">";
+  return "conv_gemm_kernel<" + std::to_string(c.bm) + ", " + std::to_string(c.bn) + ", " + std::to_string(c.bk) + ", " +
+         std::to_string(c.wm) + ", " + std::to_string(c.wn) + ", " + (s1 ? "true" : "false") + ", " +
+         (add ? "true" : "false") + ">";
+}
+
+int conv_tile_blocks(const ConvDesc& d) {
+  const Cfg c = select_cfg(d);
+  const int M = d.nimg * d.Ho * d.Wo;
+  return ((M + c.bm - 1) / c.bm) * ((d.N + c.bn - 1) / c.bn);
 }
 
 hipError_t launch_conv(const ConvDesc& d, hipStream_t s) {
   // host-side shape checks: every float4 access must stay aligned and in range
-  if (d.s0.cin % 4 || d.s0.ld % 4 || (d.s0.p2 && d.s0.ld2 % 4) || d.Kp % BK || d.ldo < d.N ||
+  if (d.s0.cin % 4 || d.s0.ld % 4 || (d.s0.p2 && d.s0.ld2 % 4) || d.Kp % KP_ALIGN || d.ldo < d.N ||
       (d.s1.p && (d.s1.cin % 4 || d.s1.ld % 4)) || d.N <= 0 || d.nimg <= 0 || d.Ho <= 0 || d.Wo <= 0 ||
       (reinterpret_cast<uintptr_t>(d.s0.p) & 15) || (reinterpret_cast<uintptr_t>(d.w) & 15) ||
       d.K > d.Kp || (d.ksplit > 1 && !d.partial))
     return hipErrorInvalidValue;
-  const int M = d.nimg * d.Ho * d.Wo;
-  // tile choice by output width N and problem size
-  if (d.N <= 32) return launch_cfg<256, 32, 4, 1>(d, s);
-  if (d.N <= 64) return launch_cfg<128, 64, 4, 1>(d, s);
-  if (M <= 4096) return launch_cfg<64, 128, 1, 4>(d, s);
-  return launch_cfg<128, 128, 2, 2>(d, s);
+  const Cfg c = select_cfg(d);
+  return c.bk == 32 ? launch_bk<32>(d, c, s) : launch_bk<16>(d, c, s);
 }
 
 }  // namespace spk

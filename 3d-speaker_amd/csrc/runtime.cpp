@@ -74,7 +74,7 @@ const Packed& Model::pack(const std::string& name, const ChanMap& out, const std
   if (it != packed.end()) return it->second;
   if (uploaded) throw SpkError(SPK_E_INVALID, "internal: pack after upload: " + name);
   const int N = out.n_phys;
-  const int Kp = round_up(K, 16);
+  const int Kp = round_up(K, 32);
   std::vector<double> wd((size_t)N * Kp, 0.0), bd(N, 0.0);
   std::map<std::string, int> seen;
   bool has_bias = false;
@@ -88,16 +88,25 @@ const Packed& Model::pack(const std::string& name, const ChanMap& out, const std
     const int nin = part.in.n_log(), cinp = part.in.n_phys;
     if (part.ci_lo + nin > cin) throw SpkError(SPK_E_WEIGHTS, part.wkey + ": in channels mismatch");
     if (part.kofs + taps * cinp > K) throw SpkError(SPK_E_INVALID, "internal: K overflow packing " + part.wkey);
-    std::vector<double> s, t;
+    std::vector<double> s, t, si, ti;
     bn_fold(part.bn, cout, s, t);
+    bn_fold(part.bn_in, cin, si, ti);
     const bool first = seen.count(part.wkey) == 0;
     seen[part.wkey] = 1;
     for (int co = 0; co < cout; ++co) {
       double* row = wd.data() + (size_t)out.phys[co] * Kp + part.kofs;
       const float* src = w.data.data() + (size_t)co * cin * taps;
+      double in_shift = 0.0;
       for (int ci = 0; ci < nin; ++ci)
-        for (int tap = 0; tap < taps; ++tap)
-          row[(size_t)tap * cinp + part.in.phys[ci]] = (double)src[(size_t)(part.ci_lo + ci) * taps + tap] * s[co];
+        for (int tap = 0; tap < taps; ++tap) {
+          const double wv = src[(size_t)(part.ci_lo + ci) * taps + tap];
+          row[(size_t)tap * cinp + part.in.phys[ci]] = wv * si[part.ci_lo + ci] * s[co];
+          in_shift += wv * ti[part.ci_lo + ci];
+        }
+      if (!part.bn_in.empty()) {
+        bd[out.phys[co]] += s[co] * in_shift;
+        has_bias = true;
+      }
     }
     if (first) {
       const HostT* cb = part.bias_key.empty() ? nullptr : &get(part.bias_key);
@@ -153,13 +162,11 @@ void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const C
   d.bias = (use_bias && p.has_bias) ? m.dptr(p.b_off) : nullptr;
   const int M = d.nimg * d.Ho * d.Wo;
   // split-K for skinny, deep GEMMs (e.g. the 20480 -> 192 embedding layer)
-  const int bm = d.N <= 32 ? 256 : (d.N <= 64 ? 128 : (M <= 4096 ? 64 : 128));
-  const int bn = d.N <= 32 ? 32 : (d.N <= 64 ? 64 : 128);
-  const int nblk = ((M + bm - 1) / bm) * ((d.N + bn - 1) / bn);
-  const int nkt = d.Kp / 16;
+  const int nblk = conv_tile_blocks(d);
+  const int nkt = d.Kp / 32;
   Buf partial;
-  if (nblk < 128 && nkt >= 64 && !io.affx && !io.gate) {
-    d.ksplit = std::max(1, std::min(nkt / 16, (256 + nblk - 1) / nblk));
+  if (nblk < 128 && nkt >= 32 && !io.affx && !io.gate) {
+    d.ksplit = std::max(1, std::min(nkt / 8, (256 + nblk - 1) / nblk));
     if (d.ksplit > 1) partial = alloc((size_t)d.ksplit * M * d.N);
   }
   ConvIO cio = io;

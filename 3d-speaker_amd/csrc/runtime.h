@@ -80,6 +80,8 @@ struct Part {
   ChanMap in;              // physical layout of the part's input source
   int ci_lo = 0;           // first logical input channel of the weight read by this part
   int kofs = 0;            // K offset of this part in the packed matrix
+  std::string bn_in;       // optional BatchNorm applied to the INPUT (linear in between), folded
+                           // as W*diag(s) and bias += W*t  (ECAPA asp_bn -> fc)
 };
 
 struct Model {

@@ -1,0 +1,17 @@
+#pragma once
+#include <algorithm>
+#include "common.h"
+
+namespace spk {
+
+hipError_t launch_time_mean(const float* x, int B, int T, int C, int ld, float* out, int ldo, hipStream_t s);
+hipError_t launch_asp_stats(const float* x, int B, int T, int C, int ld, float eps, float* out, hipStream_t s);
+hipError_t launch_attn_pool(const float* logit, int ldl, const float* x, int ldx, int B, int T, int C, float eps,
+                            float* out, hipStream_t s);
+hipError_t launch_se_apply(const float* x, int ldx, const float* gate, int ldg, const float* res, int ldr, float* out,
+                           int ldo, int B, int T, int C, hipStream_t s);
+hipError_t launch_cam_context(const float* x, int B, int T, int C, int ld, int seg, int nseg, float* out, int ldo,
+                              hipStream_t s);
+hipError_t launch_stats_pool(const float* x, int B, int T, int C, int ld, float* out, hipStream_t s);
+
+}  // namespace spk

@@ -1,0 +1,169 @@
+// Reductions and elementwise ops of the TDNN models (ECAPA-TDNN, CAM++), gfx950.
+// All tensors are channels-last [B, T, C] with pixel stride `ld`; every kernel puts one
+// lane on one channel so the time loops read coalesced 256-B rows.
+//
+//  * time_mean        SEBlock squeeze, s = mean_T(x)                       ECAPA_TDNN.py:209-216
+//  * asp_stats        global-context mean / std, weights 1/T, clamp 1e-12  ECAPA_TDNN.py:256-270
+//  * attn_pool        softmax_T(logits) weighted mean / std               ECAPA_TDNN.py:276-287
+//  * se_apply         out = x * gate[b, c] + residual                       ECAPA_TDNN.py:222, 347
+//  * cam_context      mean_T + 100-frame segment mean (ceil_mode)          campplus/layers.py:93-110
+//  * stats_pool       mean + unbiased std (no eps)                          campplus/layers.py:26-37
+#include "common.h"
+#include "tdnn_ops.h"
+
+namespace spk {
+
+namespace {
+
+inline int grid_for(long long n) { return (int)std::min<long long>((n + 255) / 256, 65536); }
+
+__global__ void time_mean_kernel(const float* __restrict__ x, int B, int T, int C, int ld, float* __restrict__ out,
+                                 int ldo) {
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C), b = (int)(e / C);
+    const float* p = x + (size_t)b * T * ld + c;
+    float s = 0.f;
+    for (int t = 0; t < T; ++t) s += p[(size_t)t * ld];
+    out[(size_t)b * ldo + c] = s / (float)T;
+  }
+}
+
+__global__ void asp_stats_kernel(const float* __restrict__ x, int B, int T, int C, int ld, float eps,
+                                 float* __restrict__ out) {
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C), b = (int)(e / C);
+    const float* p = x + (size_t)b * T * ld + c;
+    const float w = 1.0f / (float)T;
+    float mean = 0.f;
+    for (int t = 0; t < T; ++t) mean += w * p[(size_t)t * ld];
+    float q = 0.f;
+    for (int t = 0; t < T; ++t) {
+      const float d = p[(size_t)t * ld] - mean;
+      q += w * d * d;
+    }
+    out[(size_t)b * 2 * C + c] = mean;
+    out[(size_t)b * 2 * C + C + c] = sqrtf(fmaxf(q, eps));
+  }
+}
+
+__global__ void attn_pool_kernel(const float* __restrict__ logit, int ldl, const float* __restrict__ x, int ldx, int B,
+                                 int T, int C, float eps, float* __restrict__ out) {
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C), b = (int)(e / C);
+    const float* l = logit + (size_t)b * T * ldl + c;
+    const float* p = x + (size_t)b * T * ldx + c;
+    float mx = -INFINITY;
+    for (int t = 0; t < T; ++t) mx = fmaxf(mx, l[(size_t)t * ldl]);
+    float den = 0.f;
+    for (int t = 0; t < T; ++t) den += __expf(l[(size_t)t * ldl] - mx);
+    const float inv = 1.0f / den;
+    float mean = 0.f;
+    for (int t = 0; t < T; ++t) mean += (__expf(l[(size_t)t * ldl] - mx) * inv) * p[(size_t)t * ldx];
+    float q = 0.f;
+    for (int t = 0; t < T; ++t) {
+      const float d = p[(size_t)t * ldx] - mean;
+      q += (__expf(l[(size_t)t * ldl] - mx) * inv) * d * d;
+    }
+    out[(size_t)b * 2 * C + c] = mean;
+    out[(size_t)b * 2 * C + C + c] = sqrtf(fmaxf(q, eps));
+  }
+}
+
+__global__ void se_apply_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ gate, int ldg,
+                                const float* __restrict__ res, int ldr, float* __restrict__ out, int ldo, int B, int T,
+                                int C) {
+  const int C4 = C / 4;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * T * C4;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C4) * 4;
+    const long long row = e / C4;
+    const int b = (int)(row / T);
+    const float4 v = *reinterpret_cast<const float4*>(x + row * ldx + c);
+    const float4 g = *reinterpret_cast<const float4*>(gate + (size_t)b * ldg + c);
+    const float4 r = *reinterpret_cast<const float4*>(res + row * ldr + c);
+    float4 o;
+    o.x = v.x * g.x + r.x; o.y = v.y * g.y + r.y; o.z = v.z * g.z + r.z; o.w = v.w * g.w + r.w;
+    *reinterpret_cast<float4*>(out + row * ldo + c) = o;
+  }
+}
+
+// ctx[b, s, c] = mean_T(x)[b, c] + mean over frames [100 s, min(100 s + 100, T)) of x[b, :, c]
+__global__ void cam_context_kernel(const float* __restrict__ x, int B, int T, int C, int ld, int seg, int nseg,
+                                   float* __restrict__ out, int ldo) {
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C), b = (int)(e / C);
+    const float* p = x + (size_t)b * T * ld + c;
+    float tot = 0.f;
+    for (int t = 0; t < T; ++t) tot += p[(size_t)t * ld];
+    const float mean = tot / (float)T;
+    for (int s = 0; s < nseg; ++s) {
+      const int t0 = s * seg, t1 = min(T, t0 + seg);
+      float a = 0.f;
+      for (int t = t0; t < t1; ++t) a += p[(size_t)t * ld];
+      out[((size_t)b * nseg + s) * ldo + c] = mean + a / (float)(t1 - t0);
+    }
+  }
+}
+
+__global__ void stats_pool_kernel(const float* __restrict__ x, int B, int T, int C, int ld, float* __restrict__ out) {
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C), b = (int)(e / C);
+    const float* p = x + (size_t)b * T * ld + c;
+    float s = 0.f;
+    for (int t = 0; t < T; ++t) s += p[(size_t)t * ld];
+    const float mean = s / (float)T;
+    float q = 0.f;
+    for (int t = 0; t < T; ++t) {
+      const float d = p[(size_t)t * ld] - mean;
+      q += d * d;
+    }
+    out[(size_t)b * 2 * C + c] = mean;
+    out[(size_t)b * 2 * C + C + c] = sqrtf(q / (float)(T - 1));
+  }
+}
+
+}  // namespace
+
+hipError_t launch_time_mean(const float* x, int B, int T, int C, int ld, float* out, int ldo, hipStream_t s) {
+  hipLaunchKernelGGL(time_mean_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, out, ldo);
+  return hipGetLastError();
+}
+
+hipError_t launch_asp_stats(const float* x, int B, int T, int C, int ld, float eps, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(asp_stats_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, eps, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_attn_pool(const float* logit, int ldl, const float* x, int ldx, int B, int T, int C, float eps,
+                            float* out, hipStream_t s) {
+  hipLaunchKernelGGL(attn_pool_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, logit, ldl, x, ldx, B, T, C,
+                     eps, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_se_apply(const float* x, int ldx, const float* gate, int ldg, const float* res, int ldr, float* out,
+                           int ldo, int B, int T, int C, hipStream_t s) {
+  if (C % 4 || ldx % 4 || ldg % 4 || ldr % 4 || ldo % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(se_apply_kernel, dim3(grid_for((long long)B * T * C / 4)), dim3(256), 0, s, x, ldx, gate, ldg,
+                     res, ldr, out, ldo, B, T, C);
+  return hipGetLastError();
+}
+
+hipError_t launch_cam_context(const float* x, int B, int T, int C, int ld, int seg, int nseg, float* out, int ldo,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(cam_context_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, seg, nseg,
+                     out, ldo);
+  return hipGetLastError();
+}
+
+hipError_t launch_stats_pool(const float* x, int B, int T, int C, int ld, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(stats_pool_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, out);
+  return hipGetLastError();
+}
+
+}  // namespace spk

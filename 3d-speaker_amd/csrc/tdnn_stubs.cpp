@@ -6,7 +6,7 @@ namespace spk {
 hipError_t launch_cosine_affinity(const float* A, long long Na, const float* B, long long Nb, int E, float* out,
                                   long long ldo, hipStream_t s);
 
-void build_ecapa(Builder&, int) { throw SpkError(SPK_E_UNSUPPORTED, "ECAPA-TDNN plan not built yet"); }
+
 void build_campplus(Builder&, int) { throw SpkError(SPK_E_UNSUPPORTED, "CAM++ plan not built yet"); }
 
 }  // namespace spk

@@ -9,6 +9,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
+#include <algorithm>
+
+#include "../../3d-speaker_amd/csrc/tdnn_ops.h"
 
 #include "../../3d-speaker_amd/csrc/common.h"
 #include "../../3d-speaker_amd/csrc/fbank.h"
@@ -164,3 +168,81 @@ hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
 hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
 hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) { std::memset(p, v, n); return hipSuccess; }
 }
+
+// ---- TDNN reductions (contracts of csrc/tdnn_ops.h)
+namespace spk {
+hipError_t launch_time_mean(const float* x, int B, int T, int C, int ld, float* out, int ldo, hipStream_t) {
+  for (int b = 0; b < B; ++b)
+    for (int c = 0; c < C; ++c) {
+      double s = 0;
+      for (int t = 0; t < T; ++t) s += x[((size_t)b * T + t) * ld + c];
+      out[(size_t)b * ldo + c] = (float)(s / T);
+    }
+  return hipSuccess;
+}
+hipError_t launch_asp_stats(const float* x, int B, int T, int C, int ld, float eps, float* out, hipStream_t) {
+  for (int b = 0; b < B; ++b)
+    for (int c = 0; c < C; ++c) {
+      double s = 0, q = 0;
+      for (int t = 0; t < T; ++t) s += x[((size_t)b * T + t) * ld + c];
+      const double mean = s / T;
+      for (int t = 0; t < T; ++t) { const double d = x[((size_t)b * T + t) * ld + c] - mean; q += d * d / T; }
+      out[(size_t)b * 2 * C + c] = (float)mean;
+      out[(size_t)b * 2 * C + C + c] = (float)std::sqrt(std::fmax(q, (double)eps));
+    }
+  return hipSuccess;
+}
+hipError_t launch_attn_pool(const float* l, int ldl, const float* x, int ldx, int B, int T, int C, float eps,
+                            float* out, hipStream_t) {
+  std::vector<double> p(T);
+  for (int b = 0; b < B; ++b)
+    for (int c = 0; c < C; ++c) {
+      double mx = -1e300, den = 0, mean = 0, q = 0;
+      for (int t = 0; t < T; ++t) mx = std::fmax(mx, l[((size_t)b * T + t) * ldl + c]);
+      for (int t = 0; t < T; ++t) { p[t] = std::exp(l[((size_t)b * T + t) * ldl + c] - mx); den += p[t]; }
+      for (int t = 0; t < T; ++t) mean += p[t] / den * x[((size_t)b * T + t) * ldx + c];
+      for (int t = 0; t < T; ++t) { const double d = x[((size_t)b * T + t) * ldx + c] - mean; q += p[t] / den * d * d; }
+      out[(size_t)b * 2 * C + c] = (float)mean;
+      out[(size_t)b * 2 * C + C + c] = (float)std::sqrt(std::fmax(q, (double)eps));
+    }
+  return hipSuccess;
+}
+hipError_t launch_se_apply(const float* x, int ldx, const float* g, int ldg, const float* r, int ldr, float* out,
+                           int ldo, int B, int T, int C, hipStream_t) {
+  for (int b = 0; b < B; ++b)
+    for (int t = 0; t < T; ++t)
+      for (int c = 0; c < C; ++c) {
+        const size_t row = (size_t)b * T + t;
+        out[row * ldo + c] = x[row * ldx + c] * g[(size_t)b * ldg + c] + r[row * ldr + c];
+      }
+  return hipSuccess;
+}
+hipError_t launch_cam_context(const float* x, int B, int T, int C, int ld, int seg, int nseg, float* out, int ldo,
+                              hipStream_t) {
+  for (int b = 0; b < B; ++b)
+    for (int c = 0; c < C; ++c) {
+      double tot = 0;
+      for (int t = 0; t < T; ++t) tot += x[((size_t)b * T + t) * ld + c];
+      for (int s = 0; s < nseg; ++s) {
+        const int t0 = s * seg, t1 = std::min(T, t0 + seg);
+        double a = 0;
+        for (int t = t0; t < t1; ++t) a += x[((size_t)b * T + t) * ld + c];
+        out[((size_t)b * nseg + s) * ldo + c] = (float)(tot / T + a / (t1 - t0));
+      }
+    }
+  return hipSuccess;
+}
+hipError_t launch_stats_pool(const float* x, int B, int T, int C, int ld, float* out, hipStream_t) {
+  for (int b = 0; b < B; ++b)
+    for (int c = 0; c < C; ++c) {
+      double s = 0, q = 0;
+      for (int t = 0; t < T; ++t) s += x[((size_t)b * T + t) * ld + c];
+      const double mean = s / T;
+      for (int t = 0; t < T; ++t) { const double d = x[((size_t)b * T + t) * ld + c] - mean; q += d * d; }
+      out[(size_t)b * 2 * C + c] = (float)mean;
+      out[(size_t)b * 2 * C + C + c] = (float)std::sqrt(q / (T - 1));
+    }
+  return hipSuccess;
+}
+}  // namespace spk
+namespace spk { int conv_tile_blocks(const ConvDesc& d) { return (d.nimg * d.Ho * d.Wo + 127) / 128 * ((d.N + 127) / 128); } }

@@ -9,7 +9,7 @@ import helpers
 from emu_runner import EmuModel
 from oracle import models_ref
 
-EMU_ARCHS = ['eres2netv2', 'eres2net_large']
+EMU_ARCHS = ['eres2netv2', 'eres2net_large', 'ecapa']
 
 
 @pytest.mark.parametrize('arch', EMU_ARCHS)
@@ -27,3 +27,8 @@ def test_algorithmic_flops_match_survey(arch, gflop):
     """FLOPs per 2 s utterance = 2 x conv/linear MACs (forward hooks)."""
     fl = EmuModel(helpers.loaded_module(arch)).flops(198)
     assert abs(fl / 1e9 - gflop) / gflop < 2e-3, fl
+
+
+def test_ecapa_flops_match_survey():
+    fl = EmuModel(helpers.loaded_module('ecapa')).flops(198)
+    assert abs(fl / 1e9 - 7.426) / 7.426 < 2e-3, fl
