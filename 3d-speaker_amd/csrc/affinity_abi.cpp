@@ -1,4 +1,4 @@
-// Temporary: ECAPA-TDNN and CAM++ plans land in ecapa.cpp / campplus.cpp.
+// C ABI entry for the cosine-affinity kernel (affinity.hip).
 #include "runtime.h"
 
 namespace spk {
@@ -7,7 +7,7 @@ hipError_t launch_cosine_affinity(const float* A, long long Na, const float* B, 
                                   long long ldo, hipStream_t s);
 
 
-void build_campplus(Builder&, int) { throw SpkError(SPK_E_UNSUPPORTED, "CAM++ plan not built yet"); }
+
 
 }  // namespace spk
 

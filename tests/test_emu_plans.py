@@ -9,7 +9,7 @@ import helpers
 from emu_runner import EmuModel
 from oracle import models_ref
 
-EMU_ARCHS = ['eres2netv2', 'eres2net_large', 'ecapa']
+EMU_ARCHS = ['eres2netv2', 'eres2net_large', 'ecapa', 'campplus']
 
 
 @pytest.mark.parametrize('arch', EMU_ARCHS)
@@ -32,3 +32,9 @@ def test_algorithmic_flops_match_survey(arch, gflop):
 def test_ecapa_flops_match_survey():
     fl = EmuModel(helpers.loaded_module('ecapa')).flops(198)
     assert abs(fl / 1e9 - 7.426) / 7.426 < 2e-3, fl
+
+
+def test_campplus_flops_match_survey():
+    """CAM++(512) = 1.115 GMAC per 2 s utterance."""
+    fl = EmuModel(helpers.loaded_module('campplus')).flops(198)
+    assert abs(fl / 2e9 - 1.115) / 1.115 < 5e-3, fl

@@ -1,0 +1,28 @@
+#!/bin/bash
+# GPU session: tests, per-step profiles of all four models, bench, rocprofv3 stats.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+fatal() { case "$1" in 0|1) return 1;; *) return 0;; esac; }
+echo "== pytest -m gpu $(date +%T)"
+timeout -k 10 900 python -m pytest tests -m gpu -q -rf > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -6 gpurun_out/pytest_gpu.log
+if fatal $rc; then exit $rc; fi
+for a in eres2netv2 eres2net_large ecapa campplus; do
+  echo "== steps $a $(date +%T)"
+  timeout -k 10 300 python tools/profile_steps.py --arch $a --json gpurun_out/steps_$a.json > gpurun_out/steps_$a.txt 2>&1
+  rc=$?; head -12 gpurun_out/steps_$a.txt
+  if fatal $rc; then exit $rc; fi
+done
+echo "== bench $(date +%T)"
+timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log | cut -c1-600
+if fatal $rc; then exit $rc; fi
+if [ "${1:-}" = "prof" ]; then
+  echo "== rocprofv3 $(date +%T)"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
+      python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1
+  rc=$?; echo "rocprof rc=$rc"; tail -1 gpurun_out/prof.log | cut -c1-300
+fi
+echo "== done $(date +%T)"
