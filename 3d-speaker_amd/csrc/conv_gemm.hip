@@ -269,10 +269,15 @@ conv_gemm_kernel(const ConvDesc d) {
 
   // ---- epilogue, one 32x32 accumulator tile at a time through a per-wave LDS slab:
   // registers -> LDS in the MFMA C layout (col = lane&31, row = (r&3)+8(r>>2)+4(lane>>5)),
-  // then row-major sweeps (32 lanes = 128 contiguous output bytes) run the fused epilogue
-  // in a short loop instead of 16x-unrolled register code.
+  // then each lane owns 4 consecutive columns of 4 rows (8 lanes = one 128-B output row):
+  // every epilogue operand (residual, AFF inputs, bias, ...) is read as float4 and all of a
+  // tile's loads are issued before the first use, so the fused epilogue costs one memory
+  // round trip per tile instead of sixteen dependent scalar ones.
   float* ct = lds + wave * 1024;
   float* part = d.ksplit > 1 ? d.partial + (size_t)blockIdx.z * M * d.N : nullptr;
+  const bool vec = (d.N % 4 == 0) && (d.ldo % 4 == 0) && (!d.res || d.ldr % 4 == 0) &&
+                   (!d.affx || (d.ldx % 4 == 0 && d.ldy % 4 == 0)) && (!d.gate || d.gate_ld % 4 == 0) &&
+                   (!d.rowbias || d.rowbias_ld % 4 == 0);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -280,16 +285,77 @@ conv_gemm_kernel(const ConvDesc d) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) ct[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[i][j][r];
       wave_lds_sync();
-      const int n = n0 + wn * WTN + j * 32 + li;
       const int mbase = m0 + wm * WTM + i * 32;
+      const int nbase = n0 + wn * WTN + j * 32;
+      if (vec) {
+        const int c4 = (lane & 7) * 4;
+        const int n = nbase + c4;
+        f32x4 v[4], ra4[4], xa4[4], ya4[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const f32x4*>(ct + (q * 8 + (lane >> 3)) * 32 + c4);
+        if (!part && n < d.N) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int m = min(mbase + q * 8 + (lane >> 3), M - 1);
+            if (d.res) ra4[q] = *reinterpret_cast<const f32x4*>(d.res + (size_t)m * d.ldr + n);
+            if (d.affx) {
+              xa4[q] = *reinterpret_cast<const f32x4*>(d.affx + (size_t)m * d.ldx + n);
+              ya4[q] = *reinterpret_cast<const f32x4*>(d.affy + (size_t)m * d.ldy + n);
+            }
+          }
+        }
+        if (n < d.N) {
+          f32x4 bias = {0.f, 0.f, 0.f, 0.f}, ps = {1.f, 1.f, 1.f, 1.f}, pt = {0.f, 0.f, 0.f, 0.f};
+          if (!part) {
+            if (d.bias) bias = *reinterpret_cast<const f32x4*>(d.bias + n);
+            if (d.post_scale) {
+              ps = *reinterpret_cast<const f32x4*>(d.post_scale + n);
+              pt = *reinterpret_cast<const f32x4*>(d.post_shift + n);
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int m = mbase + q * 8 + (lane >> 3);
+            if (m >= M) continue;
+            if (part) {
+              *reinterpret_cast<f32x4*>(part + (size_t)m * d.N + n) = v[q];
+              continue;
+            }
+            f32x4 o = v[q] + bias;
+            if (d.rowbias) o += *reinterpret_cast<const f32x4*>(d.rowbias + (size_t)(m / (d.Ho * d.Wo)) * d.rowbias_ld + n);
+            if (d.res) o += ra4[q];
+            if (d.affx) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float t = 1.0f + tanhf(o[e]);
+                o[e] = xa4[q][e] * t + ya4[q][e] * (2.0f - t);
+              }
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                float x = apply_act(o[e], d.act);
+                if (d.post_scale) x = x * ps[e] + pt[e];
+                o[e] = apply_act(x, d.act2);
+              }
+              if (d.gate) {
+                const int wo = m % d.Wo, img = m / (d.Wo * d.Ho);
+                o *= *reinterpret_cast<const f32x4*>(d.gate + ((size_t)img * d.gate_nseg + wo / d.gate_seg) * d.gate_ld + n);
+              }
+            }
+            *reinterpret_cast<f32x4*>(d.out + (size_t)m * d.ldo + n) = o;
+          }
+        }
+      } else {
+        const int n = nbase + li;
 #pragma unroll 2
-      for (int q = 0; q < 16; ++q) {
-        const int rl = 2 * q + lh;
-        const int m = mbase + rl;
-        if (m < M && n < d.N) {
-          const float v = ct[rl * 32 + li];
-          if (part) part[(size_t)m * d.N + n] = v;
-          else d.out[(size_t)m * d.ldo + n] = epilogue_elem(d, m, n, v);
+        for (int q = 0; q < 16; ++q) {
+          const int rl = 2 * q + lh;
+          const int m = mbase + rl;
+          if (m < M && n < d.N) {
+            const float v = ct[rl * 32 + li];
+            if (part) part[(size_t)m * d.N + n] = v;
+            else d.out[(size_t)m * d.ldo + n] = epilogue_elem(d, m, n, v);
+          }
         }
       }
       wave_lds_sync();

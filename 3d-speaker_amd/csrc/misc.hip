@@ -16,36 +16,46 @@ __global__ void __launch_bounds__(256)
 stem_conv3x3_kernel(const float* __restrict__ feats, int B, int T, int F, const float* __restrict__ w,
                     const float* __restrict__ bias, int cout, int act, int wstride, float* __restrict__ out,
                     int ldo) {
-  // thread -> (pixel, 4 output channels); pixel = (b, f, t) of the (F, T) image
-  const int groups = cout / 4;
-  const long long total = (long long)B * F * T * groups;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int g = (int)(e % groups);
-    const long long pix = e / groups;
-    const int t = (int)(pix % T);
-    const int f = (int)((pix / T) % F);
-    const int b = (int)(pix / ((long long)T * F));
+  // thread -> (pixel, 16 output channels); pixel = (b, f, t) of the (F, T) image.  Weights and
+  // bias are staged in LDS once per block; 32-bit index math only.
+  __shared__ float ws[128 * 9];
+  __shared__ float bs[128];
+  for (int i = threadIdx.x; i < cout * 9; i += blockDim.x) ws[i] = w[(i / 9) * wstride + (i % 9)];
+  for (int i = threadIdx.x; i < cout; i += blockDim.x) bs[i] = bias[i];
+  __syncthreads();
+  const int groups = cout / 16;
+  const int total = B * F * T * groups;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int g = e % groups;
+    const int pix = e / groups;
+    const int t = pix % T;
+    const int bf = pix / T;
+    const int f = bf % F;
+    const int b = bf / F;
     float in[9];
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
       for (int dx = 0; dx < 3; ++dx) {
         const int ff = f + dy - 1, tt = t + dx - 1;
-        in[dy * 3 + dx] = (ff >= 0 && ff < F && tt >= 0 && tt < T) ? feats[((size_t)b * T + tt) * F + ff] : 0.f;
+        in[dy * 3 + dx] = (ff >= 0 && ff < F && tt >= 0 && tt < T) ? feats[(b * T + tt) * F + ff] : 0.f;
       }
-    float4 o;
-    float* op = &o.x;
+    float* op = out + (size_t)pix * ldo + g * 16;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = g * 4 + j;
-      float acc = 0.f;
+    for (int q = 0; q < 4; ++q) {
+      float4 o;
+      float* ov = &o.x;
 #pragma unroll
-      for (int k = 0; k < 9; ++k) acc = fmaf(in[k], w[c * wstride + k], acc);
-      acc += bias[c];
-      op[j] = act == ACT_RELU ? fmaxf(acc, 0.f) : acc;
+      for (int j = 0; j < 4; ++j) {
+        const int c = g * 16 + q * 4 + j;
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) acc = fmaf(in[k], ws[c * 9 + k], acc);
+        acc += bs[c];
+        ov[j] = act == ACT_RELU ? fmaxf(acc, 0.f) : acc;
+      }
+      *reinterpret_cast<float4*>(op + q * 4) = o;
     }
-    *reinterpret_cast<float4*>(out + pix * ldo + g * 4) = o;
   }
 }
 
@@ -79,8 +89,9 @@ tstp_kernel(const float* __restrict__ x, int B, int H, int W, int C, int ld, flo
 
 hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const float* w, const float* bias, int cout,
                                int act, int wstride, float* out, int ldo, hipStream_t s) {
-  if (cout % 4 || ldo % 4) return hipErrorInvalidValue;
-  const long long total = (long long)B * F * T * (cout / 4);
+  if (cout % 16 || cout > 128 || ldo % 4 || (long long)B * F * T * (cout / 16) >= (1LL << 31))
+    return hipErrorInvalidValue;
+  const long long total = (long long)B * F * T * (cout / 16);
   const int blocks = (int)std::min<long long>((total + 255) / 256, 65536);
   hipLaunchKernelGGL(stem_conv3x3_kernel, dim3(blocks), dim3(256), 0, s, feats, B, T, F, w, bias, cout, act, wstride, out,
                      ldo);
