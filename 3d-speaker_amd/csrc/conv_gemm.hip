@@ -74,7 +74,7 @@ __device__ __forceinline__ float epilogue_elem(const ConvDesc& d, int m, int n, 
 }
 
 template <int BM, int BN, int BK, int WM, int WN, bool S1, bool ADD>
-__global__ void __launch_bounds__(64 * WM * WN)
+__global__ void __launch_bounds__(64 * WM * WN, 4)
 conv_gemm_kernel(const ConvDesc d) {
   constexpr int NT = 64 * WM * WN;               // threads
   constexpr int WTM = BM / WM, WTN = BN / WN;    // wave tile
@@ -87,9 +87,11 @@ conv_gemm_kernel(const ConvDesc d) {
   constexpr int HK = BK / 2;                     // k values per lane half per tile
   constexpr int FQ = HK / 4;                     // f32x4 per fragment
   static_assert(TM >= 1 && TN >= 1 && BM % RPP == 0, "tile shape");
-  static_assert(2 * (BM + BN) * LDS_ROW >= WM * WN * 1024, "epilogue staging fits");
+  constexpr int LDS_STAGE = 2 * (BM + BN) * LDS_ROW;   // double-buffered A/B tiles
+  constexpr int LDS_EPI = WM * WN * TM * TN * 1024;    // every accumulator of the block
+  constexpr int LDS_FLOATS = LDS_STAGE > LDS_EPI ? LDS_STAGE : LDS_EPI;
 
-  __shared__ __attribute__((aligned(16))) float lds[2 * (BM + BN) * LDS_ROW];
+  __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
   float* As = lds;                               // [2][BM][LDS_ROW]
   float* Bs = lds + 2 * BM * LDS_ROW;            // [2][BN][LDS_ROW]
 
@@ -273,49 +275,58 @@ conv_gemm_kernel(const ConvDesc d) {
   // every epilogue operand (residual, AFF inputs, bias, ...) is read as float4 and all of a
   // tile's loads are issued before the first use, so the fused epilogue costs one memory
   // round trip per tile instead of sixteen dependent scalar ones.
-  float* ct = lds + wave * 1024;
+  // all of the wave's accumulators go to LDS first, so they are dead during the epilogue
+  float* cw = lds + wave * (TM * TN * 1024);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) cw[(i * TN + j) * 1024 + ((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[i][j][r];
+  wave_lds_sync();
   float* part = d.ksplit > 1 ? d.partial + (size_t)blockIdx.z * M * d.N : nullptr;
   const bool vec = (d.N % 4 == 0) && (d.ldo % 4 == 0) && (!d.res || d.ldr % 4 == 0) &&
                    (!d.affx || (d.ldx % 4 == 0 && d.ldy % 4 == 0)) && (!d.gate || d.gate_ld % 4 == 0) &&
                    (!d.rowbias || d.rowbias_ld % 4 == 0);
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) ct[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[i][j][r];
-      wave_lds_sync();
+#pragma unroll 1
+  for (int tile = 0; tile < TM * TN; ++tile) {
+    {
+      const int i = tile / TN, j = tile % TN;
+      const float* ct = cw + tile * 1024;
       const int mbase = m0 + wm * WTM + i * 32;
       const int nbase = n0 + wn * WTN + j * 32;
       if (vec) {
         const int c4 = (lane & 7) * 4;
         const int n = nbase + c4;
-        f32x4 v[4], ra4[4], xa4[4], ya4[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const f32x4*>(ct + (q * 8 + (lane >> 3)) * 32 + c4);
+        f32x4 bias = {0.f, 0.f, 0.f, 0.f}, ps = {1.f, 1.f, 1.f, 1.f}, pt = {0.f, 0.f, 0.f, 0.f};
         if (!part && n < d.N) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int m = min(mbase + q * 8 + (lane >> 3), M - 1);
-            if (d.res) ra4[q] = *reinterpret_cast<const f32x4*>(d.res + (size_t)m * d.ldr + n);
-            if (d.affx) {
-              xa4[q] = *reinterpret_cast<const f32x4*>(d.affx + (size_t)m * d.ldx + n);
-              ya4[q] = *reinterpret_cast<const f32x4*>(d.affy + (size_t)m * d.ldy + n);
-            }
+          if (d.bias) bias = *reinterpret_cast<const f32x4*>(d.bias + n);
+          if (d.post_scale) {
+            ps = *reinterpret_cast<const f32x4*>(d.post_scale + n);
+            pt = *reinterpret_cast<const f32x4*>(d.post_shift + n);
           }
         }
-        if (n < d.N) {
-          f32x4 bias = {0.f, 0.f, 0.f, 0.f}, ps = {1.f, 1.f, 1.f, 1.f}, pt = {0.f, 0.f, 0.f, 0.f};
-          if (!part) {
-            if (d.bias) bias = *reinterpret_cast<const f32x4*>(d.bias + n);
-            if (d.post_scale) {
-              ps = *reinterpret_cast<const f32x4*>(d.post_scale + n);
-              pt = *reinterpret_cast<const f32x4*>(d.post_shift + n);
+        // two passes of two rows: operand loads of a pass are all in flight before use
+#pragma unroll 1
+        for (int half = 0; half < 2; ++half) {
+          f32x4 v[2], ra4[2], xa4[2], ya4[2];
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int rl = (half * 2 + q) * 8 + (lane >> 3);
+            v[q] = *reinterpret_cast<const f32x4*>(ct + rl * 32 + c4);
+            if (!part && n < d.N) {
+              const int m = min(mbase + rl, M - 1);
+              if (d.res) ra4[q] = *reinterpret_cast<const f32x4*>(d.res + (size_t)m * d.ldr + n);
+              if (d.affx) {
+                xa4[q] = *reinterpret_cast<const f32x4*>(d.affx + (size_t)m * d.ldx + n);
+                ya4[q] = *reinterpret_cast<const f32x4*>(d.affy + (size_t)m * d.ldy + n);
+              }
             }
           }
+          if (n >= d.N) continue;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int m = mbase + q * 8 + (lane >> 3);
+          for (int q = 0; q < 2; ++q) {
+            const int m = mbase + (half * 2 + q) * 8 + (lane >> 3);
             if (m >= M) continue;
             if (part) {
               *reinterpret_cast<f32x4*>(part + (size_t)m * d.N + n) = v[q];
@@ -358,8 +369,8 @@ conv_gemm_kernel(const ConvDesc d) {
           }
         }
       }
-      wave_lds_sync();
     }
+  }
 }
 
 // Split-K combine: out = epi(sum_z partial[z])   (fixed z order: deterministic)
