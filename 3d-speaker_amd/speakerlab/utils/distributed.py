@@ -1,0 +1,54 @@
+"""Process-per-GPU sharding + the one collective of the path.
+
+The reference shards utterances ``wav_list[rank::nprocs]`` with no process group and
+writes files (``infer_sv_batch.py:348-350``, ``infer_diarization.py:924``).  Here the shard
+is a contiguous block (keeps output order and locality), and scoring gathers every
+rank's embeddings with ONE all-gather (RCCL over xGMI when the backend is ``nccl``),
+after which each rank scores its own row block of the N x N cosine affinity with the
+MFMA kernel — the full matrix is never materialised on one device.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous block [start, stop) of ceil(n / world) items for ``rank``."""
+    per = math.ceil(n / world) if world > 0 else n
+    start = min(n, rank * per)
+    return start, min(n, start + per)
+
+
+def all_gather_embeddings(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
+    """Gather every rank's [n_local, E] block (contiguous sharding of ``n_total`` rows) into
+    [n_total, E] on every rank.  Uneven shards are padded to ceil(n_total/world) rows."""
+    world = dist.get_world_size(group)
+    per = math.ceil(n_total / world)
+    E = local.shape[1]
+    padded = torch.zeros((per, E), dtype=local.dtype, device=local.device)
+    padded[:local.shape[0]] = local
+    if dist.get_backend(group) == 'nccl':
+        out = torch.empty((world * per, E), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(out, padded, group=group)
+        blocks = out.view(world, per, E)
+    else:
+        parts = [torch.empty_like(padded) for _ in range(world)]
+        dist.all_gather(parts, padded, group=group)
+        blocks = torch.stack(parts)
+    rows = []
+    for r in range(world):
+        s, e = shard_bounds(n_total, r, world)
+        rows.append(blocks[r, :e - s])
+    return torch.cat(rows, 0)
+
+
+def affinity_row_block(emb_all: torch.Tensor, rank: int, world: int, out: Optional[torch.Tensor] = None):
+    """(row0, [rows, N]) cosine affinity of this rank's rows against all N embeddings,
+    computed on the GPU by ``spk_cosine_affinity``."""
+    from speakerlab import _hip
+    s, e = shard_bounds(emb_all.shape[0], rank, world)
+    return s, _hip.cosine_affinity(emb_all[s:e], emb_all, out=out)

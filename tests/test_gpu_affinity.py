@@ -24,3 +24,14 @@ def test_cosine_affinity(na, nb, e):
     a[0] = 0.0   # zero row -> zeros, like sklearn
     out = _hip.cosine_affinity(torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()).cpu().numpy()
     np.testing.assert_allclose(out, ref_cos(a, b), atol=2e-6)
+
+
+def test_row_blocks_compose_full_matrix():
+    """Row-block scoring (one block per rank after the all-gather) == the full matrix."""
+    from speakerlab.utils.distributed import affinity_row_block
+    rng = np.random.default_rng(3)
+    e = torch.from_numpy(rng.standard_normal((1001, 192)).astype(np.float32)).cuda()
+    full = _hip.cosine_affinity(e).cpu().numpy()
+    blocks = [affinity_row_block(e, r, 3) for r in range(3)]
+    stacked = np.concatenate([b.cpu().numpy() for _, b in blocks])
+    np.testing.assert_allclose(stacked, full, atol=1e-6)
