@@ -1,0 +1,212 @@
+// Halo-tiled 3x3 / stride 1 / pad 1 convolution for small channel counts, fp32 MFMA, gfx950.
+//
+// Targets the Res2Net 3x3 convs of ERes2Net(V2) stages 1-2 (26 -> 26 and 52 -> 52
+// channels, physical 28 / 52; ERes2Net-large 32 / 64) and CAM++'s FCM convs, where the
+// generic implicit GEMM re-reads every input pixel nine times through L2 with 64-B
+// im2col segments.  Here a block owns an output tile of PIX pixels (TH x TW, TW chosen
+// per layer to minimise edge waste) and all NP output channels:
+//   1. the (TH+2) x (TW+2) x CIN input halo is staged into LDS once (zero outside the
+//      image, the Res2Net `sp + spx` addend summed on the way in);
+//   2. the nine taps run as nine K-slices of CIN: A fragments are read straight out of the
+//      halo at the tap offset, B (weights of one tap, [NP][CIN]) is double-buffered in LDS
+//      and the next tap's slice is prefetched into registers during the current tap;
+//   3. the fused epilogue (bias + Hardtanh / ReLU, strided write into a channel slice) is
+//      the one of the implicit-GEMM kernel (conv_epilogue.h).
+// MFMA v_mfma_f32_32x32x2_f32: lane half h owns channels [h*CIN/2, (h+1)*CIN/2) of every
+// tap (same split for A and B), read as ds_read_b64 pairs.  LDS rows are CIN+2 floats:
+// an odd number of 8-byte slots, so 32 lanes on 32 different pixels (or weight rows) hit
+// distinct banks.
+#include "common.h"
+#include "conv_epilogue.h"
+
+namespace spk {
+
+namespace {
+
+
+template <int CIN, int NP, int PIX, bool ADD>
+struct HaloCfg {
+  static constexpr int WN = NP / 32;
+  static constexpr int TILES = (PIX / 32) * WN;           // 32x32 output tiles per block
+  static constexpr int NW = TILES >= 8 ? 8 : TILES;       // waves
+  static constexpr int WM = NW / WN;
+  static constexpr int TM = (PIX / 32) / WM;              // 32-pixel tiles per wave
+  static constexpr int CS = CIN + 2;                      // LDS row stride (floats)
+  static constexpr int HC = CIN / 2;
+  static constexpr int Q = CIN / 4;                       // float4 per pixel / weight row
+  static constexpr int HALO_PIX = PIX == 256 ? 396 : 264;   // max (TH+2)(TW+2), TW in {8..64}
+  static constexpr int HALO = HALO_PIX * CS;
+  static constexpr int WBUF = NP * CS;
+  static constexpr int STAGE = HALO + 2 * WBUF;
+  static constexpr int EPI = NW * TM * 1024;
+  static constexpr int LDS = STAGE > EPI ? STAGE : EPI;
+  static constexpr int WPF = (NP * Q + 64 * NW - 1) / (64 * NW);   // weight float4 per thread
+};
+
+template <int CIN, int NP, int PIX, bool ADD>
+__global__ void __launch_bounds__(512, 2)
+conv3x3_halo_kernel(const ConvDesc d, int TW) {
+  using C = HaloCfg<CIN, NP, PIX, ADD>;
+  constexpr int NT = 64 * C::NW;
+  __shared__ __attribute__((aligned(16))) float lds[C::LDS];
+  float* halo = lds;
+  float* wbuf = lds + C::HALO;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / C::WN, wn = wave % C::WN;
+  const int li = lane & 31, lh = lane >> 5;
+  const int TH = PIX / TW, HW = TW + 2, HH = TH + 2;
+  const int H = d.Ho, W = d.Wo;
+  const int ntx = (W + TW - 1) / TW, nty = (H + TH - 1) / TH;
+  const int img = blockIdx.x / (ntx * nty);
+  const int ty = (blockIdx.x / ntx) % nty, tx = blockIdx.x % ntx;
+  const int y0 = ty * TH, x0 = tx * TW;
+
+  // ---- 1. input halo -> LDS
+  for (int idx = tid; idx < HH * HW * C::Q; idx += NT) {
+    const int q = idx % C::Q, p = idx / C::Q;
+    const int gy = y0 - 1 + p / HW, gx = x0 - 1 + p % HW;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+      const size_t pix = (size_t)(img * H + gy) * W + gx;
+      v = *reinterpret_cast<const f32x4*>(d.s0.p + pix * d.s0.ld + 4 * q);
+      if (ADD) v += *reinterpret_cast<const f32x4*>(d.s0.p2 + pix * d.s0.ld2 + 4 * q);
+    }
+    float2* dst = reinterpret_cast<float2*>(halo + p * C::CS + 4 * q);
+    dst[0] = make_float2(v[0], v[1]);
+    dst[1] = make_float2(v[2], v[3]);
+  }
+  // ---- 2. weights of tap 0 -> LDS buffer 0; later taps are prefetched through registers
+  f32x4 wr[C::WPF];
+  auto load_w = [&](int tap) {
+#pragma unroll
+    for (int r = 0; r < C::WPF; ++r) {
+      const int idx = tid + NT * r;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      const int n = idx / C::Q, q = idx % C::Q;
+      if (idx < NP * C::Q && n < d.N) v = *reinterpret_cast<const f32x4*>(d.w + (size_t)n * d.Kp + tap * CIN + 4 * q);
+      wr[r] = v;
+    }
+  };
+  auto store_w = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < C::WPF; ++r) {
+      const int idx = tid + NT * r;
+      if (idx < NP * C::Q) {
+        const int n = idx / C::Q, q = idx % C::Q;
+        float2* dst = reinterpret_cast<float2*>(wbuf + buf * C::WBUF + n * C::CS + 4 * q);
+        dst[0] = make_float2(wr[r][0], wr[r][1]);
+        dst[1] = make_float2(wr[r][2], wr[r][3]);
+      }
+    }
+  };
+  load_w(0);
+  store_w(0);
+  __syncthreads();
+
+  f32x16 acc[C::TM][1];
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][0][r] = 0.f;
+
+  // per-wave pixel rows: local pixel p -> (p / TW, p % TW) of the tile
+  int abase[C::TM];
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i) {
+    const int p = (wm * C::TM + i) * 32 + li;
+    abase[i] = ((p / TW) * HW + (p % TW)) * C::CS + lh * C::HC;
+  }
+  const int bbase = (wn * 32 + li) * C::CS + lh * C::HC;
+
+  for (int tap = 0; tap < 9; ++tap) {
+    if (tap + 1 < 9) load_w(tap + 1);
+    const int toff = ((tap / 3) * HW + (tap % 3)) * C::CS;
+    const float* wb = wbuf + (tap & 1) * C::WBUF + bbase;
+#pragma unroll
+    for (int s2 = 0; s2 < C::HC / 2; ++s2) {
+      const float2 b = *reinterpret_cast<const float2*>(wb + 2 * s2);
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i) {
+        const float2 a = *reinterpret_cast<const float2*>(halo + abase[i] + toff + 2 * s2);
+        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc[i][0], 0, 0, 0);
+        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc[i][0], 0, 0, 0);
+      }
+    }
+    if (tap + 1 < 9) store_w((tap + 1) & 1);
+    __syncthreads();
+  }
+
+  const int M = d.nimg * H * W;
+  epilogue_tiles<C::TM, 1>(d, lds, acc, wave, lane, wn * 32, M, [&](int r) {
+    const int p = wm * C::TM * 32 + r;
+    const int gy = y0 + p / TW, gx = x0 + p % TW;
+    return (gy < H && gx < W) ? (img * H + gy) * W + gx : -1;
+  });
+}
+
+template <int CIN, int NP, int PIX>
+hipError_t launch_halo_t(const ConvDesc& d, int TW, hipStream_t s) {
+  using C = HaloCfg<CIN, NP, PIX, false>;
+  const int TH = PIX / TW;
+  const int blocks = d.nimg * ((d.Ho + TH - 1) / TH) * ((d.Wo + TW - 1) / TW);
+  if (d.s0.p2)
+    hipLaunchKernelGGL((conv3x3_halo_kernel<CIN, NP, PIX, true>), dim3(blocks), dim3(64 * C::NW), 0, s, d, TW);
+  else
+    hipLaunchKernelGGL((conv3x3_halo_kernel<CIN, NP, PIX, false>), dim3(blocks), dim3(64 * C::NW), 0, s, d, TW);
+  return hipGetLastError();
+}
+
+// pixel tile size + width with the least edge waste for an H x W image
+void pick_tile(int H, int W, int np, int* pix, int* tw) {
+  double best = 1e30;
+  for (int P : {256, 128}) {
+    if (np == 32 && P == 128) continue;   // 4-wave blocks: keep 256-pixel tiles
+    for (int t : {8, 16, 32, 64}) {
+      const int th = P / t;
+      if (th < 2) continue;
+      const double cover = (double)((H + th - 1) / th) * th * ((W + t - 1) / t) * t;
+      const double cost = cover / ((double)H * W) + (P == 128 ? 0.04 : 0.0);   // small-tile halo tax
+      if (cost < best - 1e-9) { best = cost; *pix = P; *tw = t; }
+    }
+  }
+}
+
+}  // namespace
+
+bool halo_conv_supported(const ConvDesc& d) {
+  const ConvSrc& s = d.s0;
+  return s.kh == 3 && s.kw == 3 && s.sh == 1 && s.sw == 1 && s.ph == 1 && s.pw == 1 && s.dh == 1 && s.dw == 1 &&
+         !s.reflect && !s.pre_scale && !d.s1.p && d.s1.cin == 0 && d.ksplit == 1 && d.N <= 64 &&
+         (s.cin == 28 || s.cin == 32 || s.cin == 52 || s.cin == 64) && d.Ho == s.H && d.Wo == s.W &&
+         d.Kp >= 9 * s.cin && s.ld % 4 == 0 && (!s.p2 || s.ld2 % 4 == 0);
+}
+
+std::string halo_kernel_name(const ConvDesc& d) {
+  const int np = d.N <= 32 ? 32 : 64;
+  int pix = 256, tw = 16;
+  pick_tile(d.Ho, d.Wo, np, &pix, &tw);
+  const bool add = d.s0.p2 != nullptr || d.s0.ld2 > 0;
+  return "conv3x3_halo_kernel<" + std::to_string(d.s0.cin) + ", " + std::to_string(np) + ", " + std::to_string(pix) +
+         ", " + (add ? "true" : "false") + ">";
+}
+
+hipError_t launch_conv3x3_halo(const ConvDesc& d, hipStream_t s) {
+  if (!halo_conv_supported(d)) return hipErrorInvalidValue;
+  const int np = d.N <= 32 ? 32 : 64;
+  int pix = 256, tw = 16;
+  pick_tile(d.Ho, d.Wo, np, &pix, &tw);
+#define SPK_HALO_CASE(CI)                                                               \
+  if (d.s0.cin == CI) {                                                                 \
+    if (np == 32) return launch_halo_t<CI, 32, 256>(d, tw, s);                          \
+    return pix == 256 ? launch_halo_t<CI, 64, 256>(d, tw, s) : launch_halo_t<CI, 64, 128>(d, tw, s); \
+  }
+  SPK_HALO_CASE(28)
+  SPK_HALO_CASE(32)
+  SPK_HALO_CASE(52)
+  SPK_HALO_CASE(64)
+#undef SPK_HALO_CASE
+  return hipErrorInvalidValue;
+}
+
+}  // namespace spk

@@ -18,26 +18,14 @@
 #include <string>
 
 #include "common.h"
+#include "conv_epilogue.h"
 
 namespace spk {
 
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int KP_ALIGN = 32;   // weights are packed with Kp a multiple of this
-
-__device__ __forceinline__ float apply_act(float v, int act) {
-  switch (act) {
-    case ACT_RELU: return fmaxf(v, 0.0f);
-    case ACT_HTANH: return fminf(fmaxf(v, 0.0f), 20.0f);
-    case ACT_SILU: return v / (1.0f + __expf(-v));
-    case ACT_SIGMOID: return 1.0f / (1.0f + __expf(-v));
-    case ACT_TANH: return tanhf(v);
-    default: return v;
-  }
-}
 
 // XCD-aware bijective block remap: consecutive logical ids (same M tile, all N tiles) are
 // placed on one XCD so the A tile they share stays in that XCD's L2
@@ -45,32 +33,6 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 __device__ __forceinline__ int xcd_remap(int orig, int nblk) {
   const int q = nblk / 8, r = nblk % 8, xcd = orig % 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
-}
-
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// One output element of the fused epilogue (everything after the K reduction).
-__device__ __forceinline__ float epilogue_elem(const ConvDesc& d, int m, int n, float v) {
-  if (d.bias) v += d.bias[n];
-  if (d.rowbias) v += d.rowbias[(size_t)(m / (d.Ho * d.Wo)) * d.rowbias_ld + n];
-  if (d.res) v += d.res[(size_t)m * d.ldr + n];
-  if (d.affx) {
-    const float t = 1.0f + tanhf(v);
-    return d.affx[(size_t)m * d.ldx + n] * t + d.affy[(size_t)m * d.ldy + n] * (2.0f - t);
-  }
-  v = apply_act(v, d.act);
-  if (d.post_scale) v = v * d.post_scale[n] + d.post_shift[n];
-  v = apply_act(v, d.act2);
-  if (d.gate) {
-    const int wo = m % d.Wo;
-    const int img = m / (d.Wo * d.Ho);
-    v *= d.gate[((size_t)img * d.gate_nseg + wo / d.gate_seg) * d.gate_ld + n];
-  }
-  return v;
 }
 
 template <int BM, int BN, int BK, int WM, int WN, bool S1, bool ADD>
@@ -269,108 +231,8 @@ conv_gemm_kernel(const ConvDesc d) {
     }
   }
 
-  // ---- epilogue, one 32x32 accumulator tile at a time through a per-wave LDS slab:
-  // registers -> LDS in the MFMA C layout (col = lane&31, row = (r&3)+8(r>>2)+4(lane>>5)),
-  // then each lane owns 4 consecutive columns of 4 rows (8 lanes = one 128-B output row):
-  // every epilogue operand (residual, AFF inputs, bias, ...) is read as float4 and all of a
-  // tile's loads are issued before the first use, so the fused epilogue costs one memory
-  // round trip per tile instead of sixteen dependent scalar ones.
-  // all of the wave's accumulators go to LDS first, so they are dead during the epilogue
-  float* cw = lds + wave * (TM * TN * 1024);
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) cw[(i * TN + j) * 1024 + ((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[i][j][r];
-  wave_lds_sync();
-  float* part = d.ksplit > 1 ? d.partial + (size_t)blockIdx.z * M * d.N : nullptr;
-  const bool vec = (d.N % 4 == 0) && (d.ldo % 4 == 0) && (!d.res || d.ldr % 4 == 0) &&
-                   (!d.affx || (d.ldx % 4 == 0 && d.ldy % 4 == 0)) && (!d.gate || d.gate_ld % 4 == 0) &&
-                   (!d.rowbias || d.rowbias_ld % 4 == 0);
-#pragma unroll 1
-  for (int tile = 0; tile < TM * TN; ++tile) {
-    {
-      const int i = tile / TN, j = tile % TN;
-      const float* ct = cw + tile * 1024;
-      const int mbase = m0 + wm * WTM + i * 32;
-      const int nbase = n0 + wn * WTN + j * 32;
-      if (vec) {
-        const int c4 = (lane & 7) * 4;
-        const int n = nbase + c4;
-        f32x4 bias = {0.f, 0.f, 0.f, 0.f}, ps = {1.f, 1.f, 1.f, 1.f}, pt = {0.f, 0.f, 0.f, 0.f};
-        if (!part && n < d.N) {
-          if (d.bias) bias = *reinterpret_cast<const f32x4*>(d.bias + n);
-          if (d.post_scale) {
-            ps = *reinterpret_cast<const f32x4*>(d.post_scale + n);
-            pt = *reinterpret_cast<const f32x4*>(d.post_shift + n);
-          }
-        }
-        // two passes of two rows: operand loads of a pass are all in flight before use
-#pragma unroll 1
-        for (int half = 0; half < 2; ++half) {
-          f32x4 v[2], ra4[2], xa4[2], ya4[2];
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const int rl = (half * 2 + q) * 8 + (lane >> 3);
-            v[q] = *reinterpret_cast<const f32x4*>(ct + rl * 32 + c4);
-            if (!part && n < d.N) {
-              const int m = min(mbase + rl, M - 1);
-              if (d.res) ra4[q] = *reinterpret_cast<const f32x4*>(d.res + (size_t)m * d.ldr + n);
-              if (d.affx) {
-                xa4[q] = *reinterpret_cast<const f32x4*>(d.affx + (size_t)m * d.ldx + n);
-                ya4[q] = *reinterpret_cast<const f32x4*>(d.affy + (size_t)m * d.ldy + n);
-              }
-            }
-          }
-          if (n >= d.N) continue;
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const int m = mbase + (half * 2 + q) * 8 + (lane >> 3);
-            if (m >= M) continue;
-            if (part) {
-              *reinterpret_cast<f32x4*>(part + (size_t)m * d.N + n) = v[q];
-              continue;
-            }
-            f32x4 o = v[q] + bias;
-            if (d.rowbias) o += *reinterpret_cast<const f32x4*>(d.rowbias + (size_t)(m / (d.Ho * d.Wo)) * d.rowbias_ld + n);
-            if (d.res) o += ra4[q];
-            if (d.affx) {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const float t = 1.0f + tanhf(o[e]);
-                o[e] = xa4[q][e] * t + ya4[q][e] * (2.0f - t);
-              }
-            } else {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                float x = apply_act(o[e], d.act);
-                if (d.post_scale) x = x * ps[e] + pt[e];
-                o[e] = apply_act(x, d.act2);
-              }
-              if (d.gate) {
-                const int wo = m % d.Wo, img = m / (d.Wo * d.Ho);
-                o *= *reinterpret_cast<const f32x4*>(d.gate + ((size_t)img * d.gate_nseg + wo / d.gate_seg) * d.gate_ld + n);
-              }
-            }
-            *reinterpret_cast<f32x4*>(d.out + (size_t)m * d.ldo + n) = o;
-          }
-        }
-      } else {
-        const int n = nbase + li;
-#pragma unroll 2
-        for (int q = 0; q < 16; ++q) {
-          const int rl = 2 * q + lh;
-          const int m = mbase + rl;
-          if (m < M && n < d.N) {
-            const float v = ct[rl * 32 + li];
-            if (part) part[(size_t)m * d.N + n] = v;
-            else d.out[(size_t)m * d.ldo + n] = epilogue_elem(d, m, n, v);
-          }
-        }
-      }
-    }
-  }
+  // ---- fused epilogue (conv_epilogue.h): output row m of local row r is m0 + wm*WTM + r
+  epilogue_tiles<TM, TN>(d, lds, acc, wave, lane, n0 + wn * WTN, M, [&](int r) { return m0 + wm * WTM + r; });
 }
 
 // Split-K combine: out = epi(sum_z partial[z])   (fixed z order: deterministic)
@@ -428,6 +290,7 @@ hipError_t launch_bk(const ConvDesc& d, const Cfg& c, hipStream_t s) {
 
 // Name of the kernel instantiation launch_conv() picks (matches rocprofv3 kernel names).
 std::string conv_kernel_name(const ConvDesc& d) {
+  if (halo_conv_supported(d)) return halo_kernel_name(d);
   const Cfg c = select_cfg(d);
   const bool s1 = d.s1.p != nullptr || d.s1.cin > 0, add = d.s0.p2 != nullptr || d.s0.ld2 > 0;
   return "conv_gemm_kernel<" + std::to_string(c.bm) + ", " + std::to_string(c.bn) + ", " + std::to_string(c.bk) + ", " +
@@ -448,6 +311,7 @@ hipError_t launch_conv(const ConvDesc& d, hipStream_t s) {
       (reinterpret_cast<uintptr_t>(d.s0.p) & 15) || (reinterpret_cast<uintptr_t>(d.w) & 15) ||
       d.K > d.Kp || (d.ksplit > 1 && !d.partial))
     return hipErrorInvalidValue;
+  if (halo_conv_supported(d)) return launch_conv3x3_halo(d, s);
   const Cfg c = select_cfg(d);
   return c.bk == 32 ? launch_bk<32>(d, c, s) : launch_bk<16>(d, c, s);
 }
