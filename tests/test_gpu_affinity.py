@@ -35,3 +35,21 @@ def test_row_blocks_compose_full_matrix():
     blocks = [affinity_row_block(e, r, 3) for r in range(3)]
     stacked = np.concatenate([b.cpu().numpy() for _, b in blocks])
     np.testing.assert_allclose(stacked, full, atol=1e-6)
+
+
+@pytest.mark.parametrize('ctype,n', [('AHC', 30), ('spectral', 120)])
+def test_common_clustering_end_to_end(ctype, n):
+    """CommonClustering with the GPU affinity recovers well-separated synthetic speakers."""
+    from speakerlab.process.cluster import CommonClustering
+    rng = np.random.default_rng(11)
+    centers = rng.standard_normal((3, 192))
+    truth = np.repeat(np.arange(3), n // 3)
+    X = (centers[truth] + 0.25 * rng.standard_normal((n, 192))).astype(np.float32)
+    np.random.seed(0)
+    kw = dict(pval=0.1, max_num_spks=8) if ctype == 'spectral' else dict(fix_cos_thr=0.3)
+    labels = CommonClustering(ctype, mer_cos=0.8, **kw)(X)
+
+    def canon(v):
+        m = {}
+        return [m.setdefault(x, len(m)) for x in v]
+    assert canon(labels) == canon(truth)
