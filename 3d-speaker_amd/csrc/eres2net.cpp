@@ -49,9 +49,11 @@ struct ERes2Builder {
   Buf T1, CAT, MID, FB;   // block scratch, sized for the largest layer
 
   ERes2Builder(Builder& bb, bool isv2) : b(bb), m(bb.m), v2(isv2) {
-    scale = v2 ? m.cfg.scale : 2;
-    expansion = v2 ? m.cfg.expansion : 2;
-    base_width = v2 ? m.cfg.base_width : 32;
+    // ERes2Net (ERes2Net.py) fixes scale 2 / expansion 2 / baseWidth 32; ERes2Net_huge
+    // (ERes2Net_huge.py:30-152) uses 3 / 4 / 24 — taken from the config when given.
+    scale = m.cfg.scale ? m.cfg.scale : 2;
+    expansion = m.cfg.expansion ? m.cfg.expansion : 2;
+    base_width = m.cfg.base_width ? m.cfg.base_width : (v2 ? 26 : 32);
     if (scale < 1 || expansion < 1) throw SpkError(SPK_E_INVALID, "bad scale/expansion");
   }
 

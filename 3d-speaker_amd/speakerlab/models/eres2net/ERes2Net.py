@@ -32,6 +32,7 @@ class BasicBlockERes2Net_diff_AFF(Res2Block):
 
 class ERes2Net(_hip.HipModuleMixin, nn.Module):
     _hip_arch = _hip.ARCH_ERES2NET
+    _block_cfg = dict(baseWidth=32, scale=2, expansion=2)
 
     def __init__(self, block=BasicBlockERes2Net, block_fuse=BasicBlockERes2Net_diff_AFF, num_blocks=[3, 4, 6, 3],
                  m_channels=32, feat_dim=80, embedding_size=192, pooling_func='TSTP', two_emb_layer=False):
@@ -41,7 +42,7 @@ class ERes2Net(_hip.HipModuleMixin, nn.Module):
         self.feat_dim, self.embedding_size, self.two_emb_layer = feat_dim, embedding_size, two_emb_layer
         self.m_channels = m_channels
         self.stats_dim = int(feat_dim / 8) * m_channels * 8
-        m = m_channels
+        m, e = m_channels, block.expansion
         self.conv1 = nn.Conv2d(1, m, kernel_size=3, stride=1, padding=1, bias=False)
         self.bn1 = nn.BatchNorm2d(m)
         c = m
@@ -50,20 +51,23 @@ class ERes2Net(_hip.HipModuleMixin, nn.Module):
         self.layer3, c = make_stage(block_fuse, c, m * 4, num_blocks[2], 2)
         self.layer4, c = make_stage(block_fuse, c, m * 8, num_blocks[3], 2)
         self.in_planes = c
+        # three stride-2 3x3 downsamples + AFF bottom-up fusions (ERes2Net.py:178-186)
         ds = dict(kernel_size=3, stride=2, padding=1, bias=False)
-        self.layer1_downsample = nn.Conv2d(m * 2, m * 4, **ds)
-        self.layer2_downsample = nn.Conv2d(m * 4, m * 8, **ds)
-        self.layer3_downsample = nn.Conv2d(m * 8, m * 16, **ds)
-        self.fuse_mode12 = AFF(channels=m * 4)
-        self.fuse_mode123 = AFF(channels=m * 8)
-        self.fuse_mode1234 = AFF(channels=m * 16)
+        self.layer1_downsample = nn.Conv2d(m * e, m * e * 2, **ds)
+        self.layer2_downsample = nn.Conv2d(m * e * 2, m * e * 4, **ds)
+        self.layer3_downsample = nn.Conv2d(m * e * 4, m * e * 8, **ds)
+        self.fuse_mode12 = AFF(channels=m * e * 2)
+        self.fuse_mode123 = AFF(channels=m * e * 4)
+        self.fuse_mode1234 = AFF(channels=m * e * 8)
         self.n_stats = 2
-        self.pool = pooling_layers.TSTP(in_dim=self.stats_dim * 2)
-        embedding_head(self, self.stats_dim * 2, self.n_stats, embedding_size, two_emb_layer)
+        self.pool = pooling_layers.TSTP(in_dim=self.stats_dim * e)
+        embedding_head(self, self.stats_dim * e, self.n_stats, embedding_size, two_emb_layer)
 
     def _hip_config(self):
+        b = self._block_cfg
         return dict(feat_dim=self.feat_dim, embed_dim=self.embedding_size, m_channels=self.m_channels,
-                    base_width=32, scale=2, expansion=2, two_emb_layer=int(bool(self.two_emb_layer)))
+                    base_width=b['baseWidth'], scale=b['scale'], expansion=b['expansion'],
+                    two_emb_layer=int(bool(self.two_emb_layer)))
 
     def forward(self, x):
         """x: [B, T, feat_dim] float32 on a ROCm device -> [B, embedding_size]."""

@@ -110,19 +110,20 @@ def eres2netv2_forward(sd: SD, x, m_channels=64, base_width=26, scale=2, num_blo
     return emb
 
 
-def eres2net_forward(sd: SD, x, m_channels=32, num_blocks=(3, 4, 6, 3), two_emb_layer=False):
-    """ERes2Net.forward ERes2Net.py:208-231 (baseWidth 32, scale 2, expansion 2)."""
+def eres2net_forward(sd: SD, x, m_channels=32, base_width=32, scale=2, num_blocks=(3, 4, 6, 3), two_emb_layer=False):
+    """ERes2Net.forward ERes2Net.py:208-231 (baseWidth 32, scale 2, expansion 2); also
+    ERes2Net_huge.py:206-232 (baseWidth 24, scale 3, expansion 4)."""
     x = x.permute(0, 2, 1).unsqueeze(1)
     out = F.relu(_bn(F.conv2d(x, sd['conv1.weight'], padding=1), sd, 'bn1'))
-    widths = [int(math.floor(m_channels * (2 ** i) * (32 / 64.0))) for i in range(4)]
-    out1 = _eres2_layer(sd, 'layer1', out, num_blocks[0], 1, widths[0], 2, False)
-    out2 = _eres2_layer(sd, 'layer2', out1, num_blocks[1], 2, widths[1], 2, False)
+    widths = [int(math.floor(m_channels * (2 ** i) * (base_width / 64.0))) for i in range(4)]
+    out1 = _eres2_layer(sd, 'layer1', out, num_blocks[0], 1, widths[0], scale, False)
+    out2 = _eres2_layer(sd, 'layer2', out1, num_blocks[1], 2, widths[1], scale, False)
     out1_ds = F.conv2d(out1, sd['layer1_downsample.weight'], stride=2, padding=1)
     f12 = _aff(sd, 'fuse_mode12', out2, out1_ds)
-    out3 = _eres2_layer(sd, 'layer3', out2, num_blocks[2], 2, widths[2], 2, True)
+    out3 = _eres2_layer(sd, 'layer3', out2, num_blocks[2], 2, widths[2], scale, True)
     f12_ds = F.conv2d(f12, sd['layer2_downsample.weight'], stride=2, padding=1)
     f123 = _aff(sd, 'fuse_mode123', out3, f12_ds)
-    out4 = _eres2_layer(sd, 'layer4', out3, num_blocks[3], 2, widths[3], 2, True)
+    out4 = _eres2_layer(sd, 'layer4', out3, num_blocks[3], 2, widths[3], scale, True)
     f123_ds = F.conv2d(f123, sd['layer3_downsample.weight'], stride=2, padding=1)
     f1234 = _aff(sd, 'fuse_mode1234', out4, f123_ds)
     emb = F.linear(_tstp(f1234), sd['seg_1.weight'], sd['seg_1.bias'])
@@ -278,6 +279,13 @@ ARCHS = {
                        dict(feat_dim=80, embedding_size=192, m_channels=64)),
     'ecapa': (ecapa_forward, dict(input_size=80, lin_neurons=192, channels=[1024, 1024, 1024, 1024, 3072])),
     'campplus': (campplus_forward, dict(feat_dim=80, embedding_size=512)),
+    'eres2net_huge': (lambda sd, x: eres2net_forward(sd, x, m_channels=64, base_width=24, scale=3),
+                      dict(feat_dim=80, embedding_size=192)),
+    'eres2netv2_w24s4ep4': (lambda sd, x: eres2netv2_forward(sd, x, base_width=24, scale=4),
+                            dict(feat_dim=80, embedding_size=192, baseWidth=24, scale=4, expansion=4)),
+    'campplus_192': (campplus_forward, dict(feat_dim=80, embedding_size=192)),
+    'eres2net_base': (lambda sd, x: eres2net_forward(sd, x, m_channels=32), dict(feat_dim=80, embedding_size=512,
+                                                                                  m_channels=32)),
 }
 
 

@@ -51,6 +51,7 @@ fbank_ref = _load('_fbank_ref', os.path.join(REPO, 'oracle', 'fbank_ref.py'))
 sys.path.insert(0, REF)
 from speakerlab.models.eres2net.ERes2NetV2 import ERes2NetV2  # noqa: E402
 from speakerlab.models.eres2net.ERes2Net import ERes2Net  # noqa: E402
+from speakerlab.models.eres2net.ERes2Net_huge import ERes2Net as ERes2NetHuge  # noqa: E402
 from speakerlab.models.ecapa_tdnn.ECAPA_TDNN import ECAPA_TDNN  # noqa: E402
 from speakerlab.models.campplus.DTDNN import CAMPPlus  # noqa: E402
 from speakerlab.utils import score_metrics  # noqa: E402
@@ -60,6 +61,11 @@ ARCHS = {
     'eres2net_large': (ERes2Net, dict(feat_dim=80, embedding_size=192, m_channels=64)),
     'ecapa': (ECAPA_TDNN, dict(input_size=80, lin_neurons=192, channels=[1024, 1024, 1024, 1024, 3072])),
     'campplus': (CAMPPlus, dict(feat_dim=80, embedding_size=512)),
+    # registry variants on the same kernels
+    'eres2net_huge': (ERes2NetHuge, dict(feat_dim=80, embedding_size=192)),
+    'eres2netv2_w24s4ep4': (ERes2NetV2, dict(feat_dim=80, embedding_size=192, baseWidth=24, scale=4, expansion=4)),
+    'campplus_192': (CAMPPlus, dict(feat_dim=80, embedding_size=192)),
+    'eres2net_base': (ERes2Net, dict(feat_dim=80, embedding_size=512, m_channels=32)),
 }
 
 # (batch, samples) per golden set: 2 s, 1.5 s, 1 s  ->  T = 198, 148, 98 frames

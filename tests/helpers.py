@@ -8,6 +8,7 @@ import torch
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 ARCHS = ['eres2netv2', 'eres2net_large', 'ecapa', 'campplus']
+VARIANTS = ['eres2net_huge', 'eres2netv2_w24s4ep4', 'campplus_192', 'eres2net_base']
 
 
 def product_module(arch):
@@ -23,6 +24,18 @@ def product_module(arch):
     if arch == 'campplus':
         from speakerlab.models.campplus.DTDNN import CAMPPlus
         return CAMPPlus(feat_dim=80, embedding_size=512)
+    if arch == 'eres2net_huge':
+        from speakerlab.models.eres2net.ERes2Net_huge import ERes2Net as Huge
+        return Huge(feat_dim=80, embedding_size=192)
+    if arch == 'eres2netv2_w24s4ep4':
+        from speakerlab.models.eres2net.ERes2NetV2 import ERes2NetV2
+        return ERes2NetV2(feat_dim=80, embedding_size=192, baseWidth=24, scale=4, expansion=4)
+    if arch == 'campplus_192':
+        from speakerlab.models.campplus.DTDNN import CAMPPlus
+        return CAMPPlus(feat_dim=80, embedding_size=192)
+    if arch == 'eres2net_base':
+        from speakerlab.models.eres2net.ERes2Net import ERes2Net
+        return ERes2Net(feat_dim=80, embedding_size=512, m_channels=32)
     raise KeyError(arch)
 
 

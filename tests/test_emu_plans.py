@@ -9,7 +9,7 @@ import helpers
 from emu_runner import EmuModel
 from oracle import models_ref
 
-EMU_ARCHS = ['eres2netv2', 'eres2net_large', 'ecapa', 'campplus']
+EMU_ARCHS = helpers.ARCHS + helpers.VARIANTS
 
 
 @pytest.mark.parametrize('arch', EMU_ARCHS)
@@ -19,7 +19,8 @@ def test_emulated_plan_matches_oracle(arch):
     feats = torch.from_numpy(g['feats2'][:1])          # 1 x 98 frames keeps the loops quick
     ref = g['emb64_2'][:1]
     emb = EmuModel(m)(feats).numpy()
-    assert helpers.rel_err(emb, ref).max() < 1e-4
+    floor = helpers.rel_err(g['emb32_2'][:1], ref).max()     # the reference's own fp32 noise
+    assert helpers.rel_err(emb, ref).max() < max(1e-4, 2 * floor)
 
 
 @pytest.mark.parametrize('arch,gflop', [('eres2netv2', 16.533), ('eres2net_large', 26.747)])

@@ -10,7 +10,7 @@ from oracle import models_ref
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
-GPU_ARCHS = ['eres2netv2', 'eres2net_large', 'ecapa', 'campplus']
+GPU_ARCHS = helpers.ARCHS + helpers.VARIANTS
 
 _cache = {}
 
@@ -31,11 +31,14 @@ def test_golden_embeddings(arch):
         assert emb.shape == g[f'emb32_{i}'].shape
         e64 = helpers.rel_err(emb, g[f'emb64_{i}']).max()
         e32 = helpers.rel_err(emb, g[f'emb32_{i}']).max()
-        print(f'{arch} set{i}: rel err vs fp64 {e64:.2e}, vs reference fp32 {e32:.2e}')
-        assert e64 < TOL and e32 < TOL, (arch, i, e64, e32)
+        # variants with a reference fp32-vs-fp64 floor above the bar (w24s4ep4: 5e-4 with
+        # random weights) are held to 2x that floor; the four north-star models to 1e-4
+        tol = max(TOL, 2 * helpers.rel_err(g[f'emb32_{i}'], g[f'emb64_{i}']).max())
+        print(f'{arch} set{i}: rel err vs fp64 {e64:.2e}, vs reference fp32 {e32:.2e} (tol {tol:.1e})')
+        assert e64 < tol and e32 < tol, (arch, i, e64, e32)
 
 
-@pytest.mark.parametrize('arch', GPU_ARCHS)
+@pytest.mark.parametrize('arch', helpers.ARCHS)
 @pytest.mark.parametrize('B,T', [(1, 57), (5, 101), (33, 198)])
 def test_ragged_shapes_vs_oracle(arch, B, T):
     torch.manual_seed(B * 1000 + T)

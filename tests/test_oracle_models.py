@@ -8,14 +8,16 @@ import helpers
 from oracle import models_ref
 
 
-@pytest.mark.parametrize('arch', helpers.ARCHS)
+@pytest.mark.parametrize('arch', helpers.ARCHS + helpers.VARIANTS)
 def test_oracle_matches_reference_fp32(arch):
     g = helpers.golden(arch)
     sd = helpers.state_dict(arch)
     for i in range(3):
         emb = models_ref.forward(arch, sd, torch.from_numpy(g[f'feats{i}'])).numpy()
         # same op sequence in fp32: only summation-order noise
-        assert helpers.rel_err(emb, g[f'emb32_{i}']).max() < 2e-6, (arch, i)
+        # same op sequence in fp32: only summation-order noise (x reference conditioning)
+        floor = helpers.rel_err(g[f'emb32_{i}'], g[f'emb64_{i}']).max()
+        assert helpers.rel_err(emb, g[f'emb32_{i}']).max() < max(2e-6, 0.2 * floor), (arch, i)
 
 
 @pytest.mark.parametrize('arch', ['eres2netv2', 'campplus'])

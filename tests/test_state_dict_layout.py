@@ -8,7 +8,7 @@ import pytest
 import helpers
 
 
-@pytest.mark.parametrize('arch', helpers.ARCHS)
+@pytest.mark.parametrize('arch', helpers.ARCHS + helpers.VARIANTS)
 def test_keys_and_shapes_match_reference(arch):
     ref = helpers.ref_keys(arch)
     mine = {k: list(v.shape) for k, v in helpers.product_module(arch).state_dict().items()}
@@ -22,6 +22,7 @@ def test_keys_and_shapes_match_reference(arch):
     'speakerlab.models.eres2net.ERes2Net.ERes2Net',
     'speakerlab.models.ecapa_tdnn.ECAPA_TDNN.ECAPA_TDNN',
     'speakerlab.models.campplus.DTDNN.CAMPPlus',
+    'speakerlab.models.eres2net.ERes2Net_huge.ERes2Net',
 ])
 def test_registry_dotted_paths_import(dotted):
     mod, _, cls = dotted.rpartition('.')
