@@ -48,7 +48,6 @@ void build_campplus(Builder& b, int T) {
   const int F = m.cfg.feat_dim;
   const int mc = (int)m.dim("head.conv1.weight", 0);
   if (F % 8 || mc % 4) throw SpkError(SPK_E_UNSUPPORTED, "CAM++: feat_dim % 8 and m_channels % 4 required");
-  const double Td = T;
   // ---- FCM stem
   const Packed& stem = m.pack("head.conv1", ChanMap::dense(mc),
                               {Part{"head.conv1.weight", "", "head.bn1", ChanMap::dense(1, 1), 0, 0}}, 9);
@@ -78,7 +77,10 @@ void build_campplus(Builder& b, int T) {
       std::vector<Part> parts{Part{p + ".conv2.weight", "", p + ".bn2", cm, 0, 0}};
       if (sc) parts.push_back(Part{p + ".shortcut.0.weight", "", p + ".shortcut.1", cm, 0, 9 * mc});
       const Packed& c2 = m.pack(p + ".conv2", cm, parts, 9 * mc + (sc ? mc : 0));
-      b.macs_per_utt += (double)Ho * T * mc * mc * 9 * 2 + (sc ? (double)Ho * T * mc * mc : 0.0);
+      const double macs1 = (double)Ho * T * mc * mc * 9;
+      const double macs2 = macs1 + (sc ? (double)Ho * T * mc * mc : 0.0);
+      b.macs_per_utt += macs1;
+      if (!b.plan) b.macs_per_utt += macs2;
       if (b.plan) {
         ConvDesc d;
         d.nimg = B; d.Ho = Ho; d.Wo = T;
@@ -86,6 +88,7 @@ void build_campplus(Builder& b, int T) {
         d.ldo = mc; d.act = ACT_RELU;
         Builder::ConvIO io; io.s0 = x.buf; io.out = y1.buf;
         b.conv(p + ".conv1", d, c1, io);
+        b.macs_per_utt += macs2;
         ConvDesc e;
         e.nimg = B; e.Ho = Ho; e.Wo = T;
         e.s0 = src2d(y1, mc, 3, 3, 1, 1, 1, 1);
@@ -204,8 +207,13 @@ void build_campplus(Builder& b, int T) {
       const int ks = (int)m.dim(c + ".linear_local.weight", 2);
       const Packed& loc = m.pack(c + ".linear_local", ChanMap::dense(growth),
                                  {Part{c + ".linear_local.weight", "", "", ChanMap::dense(bnc), 0, 0}}, ks * bnc);
-      b.macs_per_utt += T2d * bnc * cin + T2d * red * bnc + T2d * growth * red + T2d * growth * bnc * ks;
-      if (!b.plan) continue;
+      // reference-algorithmic MACs (the reference runs the CAM linears on every frame)
+      const double m_l1 = T2d * bnc * cin, m_c1 = T2d * red * bnc, m_c2 = T2d * growth * red;
+      const double m_loc = T2d * growth * bnc * ks;
+      if (!b.plan) {
+        b.macs_per_utt += m_l1 + m_c1 + m_c2 + m_loc;
+        continue;
+      }
       const A4 db{bk.buf, bk.c_fin, 1, T2, bk.c_fin};
       {
         ConvDesc d;
@@ -215,6 +223,7 @@ void build_campplus(Builder& b, int T) {
         d.s0.pre_shift = m.dptr(pre->pt_off);
         d.ldo = bnc; d.act = ACT_RELU;
         Builder::ConvIO io; io.s0 = bk.buf; io.out = Hh;
+        b.macs_per_utt += m_l1;
         b.conv(q + ".linear1", d, l1, io);
       }
       b.step(c + ".context", [=](const Ctx& cx) {
@@ -227,6 +236,7 @@ void build_campplus(Builder& b, int T) {
         d.s0 = s;
         d.ldo = red; d.act = ACT_RELU;
         Builder::ConvIO io; io.s0 = CTX; io.out = CM;
+        b.macs_per_utt += m_c1;
         b.conv(c + ".linear1", d, cl1, io);
         ConvDesc e;
         e.nimg = B * nseg; e.Ho = 1; e.Wo = 1;
@@ -234,6 +244,7 @@ void build_campplus(Builder& b, int T) {
         e.s0 = s2;
         e.ldo = growth; e.act = ACT_SIGMOID;
         Builder::ConvIO io2; io2.s0 = CM; io2.out = GATE;
+        b.macs_per_utt += m_c2;
         b.conv(c + ".linear2", e, cl2, io2);
       }
       {
@@ -244,6 +255,7 @@ void build_campplus(Builder& b, int T) {
         d.ldo = bk.c_fin;
         d.gate_ld = growth; d.gate_seg = 100; d.gate_nseg = nseg;
         Builder::ConvIO io; io.s0 = Hh; io.out = bk.buf.at((size_t)cin); io.gate = GATE;
+        b.macs_per_utt += m_loc;
         b.conv(c + ".linear_local", d, loc, io);
       }
     }

@@ -246,14 +246,18 @@ void build_ecapa(Builder& b, int T) {
   const Packed* pan = post("asp.tdnn.norm.norm", att);
   const Packed& patt2 = m.pack("asp.conv", ChanMap::dense(Cm),
                                {Part{"asp.conv.conv.weight", "asp.conv.conv.bias", "", ChanMap::dense(att), 0, 0}}, att);
-  b.macs_per_utt += Td * att * 3.0 * Cm + Td * Cm * att;
+  // reference-algorithmic MACs (the context half of asp.tdnn is computed once per utterance)
+  const double macs_ctx = Td * att * 2.0 * Cm, macs_att = Td * att * (double)Cm, macs_conv = Td * Cm * (double)att;
   const int E = (int)m.dim("fc.conv.weight", 0);
   if (E % 4) throw SpkError(SPK_E_UNSUPPORTED, "lin_neurons must be a multiple of 4");
   Part fcp{"fc.conv.weight", "fc.conv.bias", "", ChanMap::dense(2 * Cm), 0, 0};
   fcp.bn_in = "asp_bn.norm";
   const Packed& pfc = m.pack("fc", ChanMap::dense(E, 1), {fcp}, 2 * Cm);
-  b.macs_per_utt += (double)E * 2 * Cm;
-  if (!b.plan) return;
+  const double macs_fc = (double)E * 2 * Cm;
+  if (!b.plan) {
+    b.macs_per_utt += macs_ctx + macs_att + macs_conv + macs_fc;
+    return;
+  }
   b.step("asp.stats", [=](const Ctx& c) { return launch_asp_stats(c.resolve(A), B, T, Cm, Cm, 1e-12f, c.resolve(MS), c.stream); });
   {
     ConvDesc d;
@@ -261,6 +265,7 @@ void build_ecapa(Builder& b, int T) {
     d.s0 = src_vec(2 * Cm);
     d.ldo = att;
     Builder::ConvIO io; io.s0 = MS; io.out = CB;
+    b.macs_per_utt += macs_ctx;
     b.conv("asp.tdnn.ctx", d, pctx, io, /*use_bias=*/false);
   }
   {
@@ -271,6 +276,7 @@ void build_ecapa(Builder& b, int T) {
     d.rowbias_ld = att;
     set_post(d, pan);
     Builder::ConvIO io; io.s0 = A; io.out = HA; io.rowbias = CB;
+    b.macs_per_utt += macs_att;
     b.conv("asp.tdnn", d, patt, io);
   }
   {
@@ -279,6 +285,7 @@ void build_ecapa(Builder& b, int T) {
     d.s0 = src1d(att, T, att);
     d.ldo = Cm;
     Builder::ConvIO io; io.s0 = HA; io.out = L;
+    b.macs_per_utt += macs_conv;
     b.conv("asp.conv", d, patt2, io);
   }
   b.step("asp.pool", [=](const Ctx& c) {
@@ -290,6 +297,7 @@ void build_ecapa(Builder& b, int T) {
     d.s0 = src_vec(2 * Cm);
     d.ldo = E;
     Builder::ConvIO io; io.s0 = P; io.out = Buf{Buf::OUT, 0, nullptr};
+    b.macs_per_utt += macs_fc;
     b.conv("fc", d, pfc, io);
   }
 }

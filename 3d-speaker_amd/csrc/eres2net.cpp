@@ -72,8 +72,12 @@ struct ERes2Builder {
     const Packed& a1 = m.pack(p + ".la3", xin,
                               {Part{p + ".local_att.3.weight", p + ".local_att.3.bias", p + ".local_att.4", mid, 0, 0}},
                               mid.n_phys);
-    b.macs_per_utt += pix(x) * (2.0 * C * inter + (double)inter * C);
-    if (!b.plan) return;
+    const double m0 = pix(x) * 2.0 * C * inter, m3 = pix(x) * (double)inter * C;
+    if (!b.plan) {
+      b.macs_per_utt += m0 + m3;
+      return;
+    }
+    b.macs_per_utt += m0;
     ConvDesc d;
     d.nimg = b.B; d.Ho = x.H; d.Wo = x.W;
     d.s0 = src_of(nullptr, x, cp, 1, 1, 0);
@@ -90,6 +94,7 @@ struct ERes2Builder {
     e.ldo = out.ld; e.ldx = x.ld; e.ldy = y.ld;
     Builder::ConvIO io2;
     io2.s0 = MID; io2.out = out.buf; io2.affx = x.buf; io2.affy = y.buf;
+    b.macs_per_utt += m3;
     b.conv(p + ".local_att.3", e, a1, io2);
   }
 
@@ -113,7 +118,6 @@ struct ERes2Builder {
       Builder::ConvIO io; io.s0 = x.buf; io.out = T1;
       b.conv(p + ".conv1", d, c1, io);
     }
-    const T4 t1{T1, ldt, Ho, Wo, ldt};
     const T4 cat{CAT, ldt, Ho, Wo, ldt};
     for (int i = 0; i < scale; ++i) {
       T4 in{T1.at((size_t)i * wp), ldt, Ho, Wo, wp};

@@ -75,9 +75,10 @@ class EmuModel:
         steps = []
         for i in range(n.value):
             name = ctypes.create_string_buffer(256)
+            kern = ctypes.create_string_buffer(256)
             fl = ctypes.c_double()
-            _check(lib().spk_model_plan_step(self.handle, B, T, i, name, 256, None, 0, ctypes.byref(fl)), 'step')
-            steps.append((name.value.decode(), fl.value))
+            _check(lib().spk_model_plan_step(self.handle, B, T, i, name, 256, kern, 256, ctypes.byref(fl)), 'step')
+            steps.append((name.value.decode(), fl.value, kern.value.decode()))
         return steps
 
     def flops(self, T):

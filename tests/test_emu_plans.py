@@ -39,3 +39,16 @@ def test_campplus_flops_match_survey():
     """CAM++(512) = 1.115 GMAC per 2 s utterance."""
     fl = EmuModel(helpers.loaded_module('campplus')).flops(198)
     assert abs(fl / 2e9 - 1.115) / 1.115 < 5e-3, fl
+
+
+@pytest.mark.parametrize('arch', helpers.ARCHS)
+def test_flops_attributed_per_step(arch):
+    """Per-step FLOPs (used for the per-kernel roofline) add up to the model total and land
+    on the GEMM / conv launch that performs them."""
+    em = EmuModel(helpers.loaded_module(arch))
+    steps = em.plan(2, 198)
+    total = sum(f for _, f, _ in steps)
+    assert abs(total - 2 * em.flops(198)) / total < 1e-9
+    for name, f, kern in steps:
+        if kern.startswith(('conv_gemm', 'conv3x3')):
+            assert f > 0, (name, kern)
