@@ -122,3 +122,29 @@ def load_synthetic_weights(module, seed: int = 0, bn_stats: Mapping[str, np.ndar
 def pcm16_batch(n_utts: int, n_samples: int, seed: int) -> np.ndarray:
     """[n_utts, n_samples] float32 batch; utterance i uses seed ``seed * 1_000_000 + i``."""
     return np.stack([synth_wav(n_samples, seed * 1_000_000 + i) for i in range(n_utts)])
+
+
+def synth_meeting(seconds: float, n_speakers: int, seed: int, turn=(1.0, 8.0), silence=0.1):
+    """Synthetic meeting: random speaker turns of ``turn`` seconds from
+    ``n_speakers`` fixed-timbre synthetic speakers, ~``silence`` fraction of pauses.
+    Returns (wav float32 [L], turns [[st, ed, speaker], ...])."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    total = int(seconds * SAMPLE_RATE)
+    wav = np.zeros(total, dtype=np.float32)
+    turns, pos, k, prev = [], 0, 0, -1
+    while pos < total:
+        if rng.uniform() < silence:
+            pos += int(rng.uniform(0.2, 1.0) * SAMPLE_RATE)
+            continue
+        spk = int(rng.integers(n_speakers))
+        if spk == prev:
+            spk = (spk + 1) % n_speakers
+        n = min(int(rng.uniform(*turn) * SAMPLE_RATE), total - pos)
+        if n <= 0:
+            break
+        wav[pos:pos + n] = synth_wav(n, seed * 100_003 + k, speaker=spk)
+        turns.append([pos / SAMPLE_RATE, (pos + n) / SAMPLE_RATE, spk])
+        pos += n
+        k += 1
+        prev = spk
+    return wav, turns

@@ -40,3 +40,20 @@ def test_registry_specs_build(model_id):
     spec = isb.supports[model_id]['model']
     m = dynamic_import(spec['obj'])(**spec['args'])
     assert sum(p.numel() for p in m.parameters()) > 1e6
+
+
+def test_score_trials_parse(tmp_path):
+    from speakerlab.bin import compute_score_metrics as csm
+    p = tmp_path / 't'
+    p.write_text('a b target\nc d nontarget\n\ne f 1\ng h 0\n')
+    pairs, labels = csm.parse_trials(p)
+    assert labels.tolist() == [1, 0, 1, 0] and pairs[2][:2] == ['e', 'f']
+    p.write_text('a b maybe\n')
+    with pytest.raises(Exception):
+        csm.parse_trials(p)
+
+
+def test_diarization_cli_parser():
+    from speakerlab.bin import infer_diarization as idz
+    a = idz.parser.parse_args(['--wav', 'x.wav', '--out_dir', 'o'])
+    assert (a.chunk_dur, a.chunk_step, a.batch_size, a.cluster_mer_cos, a.vad_min_speech_ms) == (1.5, 0.75, 64, 0.3, 200.0)

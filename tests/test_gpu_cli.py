@@ -1,0 +1,57 @@
+"""infer_sv_batch end to end on the GPU: wav files -> 10 s circle-padded chunks -> GPU Fbank
+-> native forward -> per-wav mean, checked against the oracle (fp64 Fbank + fp64 model)
+on the same chunks (reference ``speakerlab/bin/infer_sv_batch.py:122-207, 300-330``)."""
+import numpy as np
+import pytest
+import torch
+
+import helpers
+from oracle import fbank_ref, models_ref
+from speakerlab.bin import infer_sv_batch as isb
+from speakerlab.utils import kaldi_io, synthetic
+from speakerlab.utils.fileio import write_wav
+
+pytestmark = pytest.mark.gpu
+
+MODEL_ID = 'iic/speech_campplus_sv_zh-cn_16k-common'      # CAM++(192): cheap in the fp64 oracle
+
+
+def _wavs(tmp_path):
+    paths = []
+    for i, sec in enumerate([3, 12, 21, 0.5]):
+        p = tmp_path / f'spk{i}.wav'
+        write_wav(str(p), synthetic.synth_wav(int(sec * 16000), seed=40 + i) / 32768.0)
+        paths.append(str(p))
+    lst = tmp_path / 'wav.list'
+    lst.write_text('\n'.join(paths) + '\n')
+    return paths, lst
+
+
+def _oracle(paths):
+    class A:
+        synthetic_weights = True
+    sd = isb.build_model(isb.supports[MODEL_ID], A, None).state_dict()
+    out = {}
+    for p in paths:
+        chunks = isb.load_wav_chunks(p).numpy()
+        feats = torch.from_numpy(fbank_ref.fbank_batch(chunks))
+        out[isb.wav_id_of(p)] = models_ref.forward('campplus_192', sd, feats).numpy().mean(0)
+    return out
+
+
+@pytest.mark.parametrize('fmt', ['npy', 'ark'])
+def test_infer_sv_batch_matches_oracle(tmp_path, fmt):
+    paths, lst = _wavs(tmp_path)
+    out_dir = tmp_path / 'emb'
+    isb.main(['--model_id', MODEL_ID, '--wavs', str(lst), '--feat_out_dir', str(out_dir), '--synthetic_weights',
+              '--feat_out_format', fmt, '--batch_size', '2', '--diable_progress_bar', '--nprocs', '1'])
+    if fmt == 'npy':
+        got = {isb.wav_id_of(p): np.load(out_dir / f'{isb.wav_id_of(p)}.npy') for p in paths}
+    else:
+        got = dict(kaldi_io.read_ark(str(out_dir / 'embedding_0.ark')))
+    ref = _oracle(paths)
+    assert sorted(got) == sorted(ref)
+    for k in ref:
+        assert got[k].shape == (192,)
+        # end to end includes the fp32 FFT noise of the Fbank (tests/test_gpu_fbank.py)
+        assert helpers.rel_err(got[k][None], ref[k][None]).max() < 5e-4, k
