@@ -84,7 +84,8 @@ def roofline(model, feats, device, traffic_json):
     traffic = None
     if traffic_json and os.path.exists(traffic_json):
         try:
-            traffic = json.load(open(traffic_json)).get(kern)
+            t = json.load(open(traffic_json)).get(kern)
+            traffic = None if t is None else round(t['bytes_per_launch'])
         except Exception:
             traffic = None
     return {
@@ -95,6 +96,7 @@ def roofline(model, feats, device, traffic_json):
         'unit': 'TFLOP/s',
         'frac': round(achieved / PEAK_FP32_TFLOPS, 4),
         'traffic': traffic,
+        'traffic_unit': 'HBM bytes per launch (rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE, KiB -> B)',
         'launches_per_step': g['launches'],
         'avg_launch_ms': round(avg_ms, 4),
         'flops_per_launch': flops_per_launch,
