@@ -34,7 +34,7 @@ struct HaloCfg {
   static constexpr int CS = CIN + 2;                      // LDS row stride (floats)
   static constexpr int HC = CIN / 2;
   static constexpr int Q = CIN / 4;                       // float4 per pixel / weight row
-  static constexpr int HALO_PIX = PIX == 256 ? 396 : 264;   // max (TH+2)(TW+2), TW in {8..64}
+  static constexpr int HALO_PIX = PIX == 256 ? 340 : 204;   // max (TH+2)(TW+2), TW in {8, 16, 32}
   static constexpr int HALO = HALO_PIX * CS;
   static constexpr int WBUF = NP * CS;
   static constexpr int STAGE = HALO + 2 * WBUF;
@@ -62,19 +62,34 @@ conv3x3_halo_kernel(const ConvDesc d, int TW) {
   const int ty = (blockIdx.x / ntx) % nty, tx = blockIdx.x % ntx;
   const int y0 = ty * TH, x0 = tx * TW;
 
-  // ---- 1. input halo -> LDS
-  for (int idx = tid; idx < HH * HW * C::Q; idx += NT) {
-    const int q = idx % C::Q, p = idx / C::Q;
-    const int gy = y0 - 1 + p / HW, gx = x0 - 1 + p % HW;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-      const size_t pix = (size_t)(img * H + gy) * W + gx;
-      v = *reinterpret_cast<const f32x4*>(d.s0.p + pix * d.s0.ld + 4 * q);
-      if (ADD) v += *reinterpret_cast<const f32x4*>(d.s0.p2 + pix * d.s0.ld2 + 4 * q);
+  // ---- 1. input halo -> LDS: batches of HB float4 per thread, every load of a batch in
+  //         flight before the first LDS write (one memory round trip per batch)
+  constexpr int HB = ADD ? 4 : 8;
+  const int hq = HH * HW * C::Q;
+  for (int base = 0; base < hq; base += NT * HB) {
+    f32x4 v[HB];
+#pragma unroll
+    for (int r = 0; r < HB; ++r) {
+      const int idx = base + tid + NT * r;
+      v[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int q = idx % C::Q, p = idx / C::Q;
+      const int gy = y0 - 1 + p / HW, gx = x0 - 1 + p % HW;
+      if (idx < hq && gy >= 0 && gy < H && gx >= 0 && gx < W) {
+        const size_t pix = (size_t)(img * H + gy) * W + gx;
+        v[r] = *reinterpret_cast<const f32x4*>(d.s0.p + pix * d.s0.ld + 4 * q);
+        if (ADD) v[r] += *reinterpret_cast<const f32x4*>(d.s0.p2 + pix * d.s0.ld2 + 4 * q);
+      }
     }
-    float2* dst = reinterpret_cast<float2*>(halo + p * C::CS + 4 * q);
-    dst[0] = make_float2(v[0], v[1]);
-    dst[1] = make_float2(v[2], v[3]);
+#pragma unroll
+    for (int r = 0; r < HB; ++r) {
+      const int idx = base + tid + NT * r;
+      if (idx < hq) {
+        const int q = idx % C::Q, p = idx / C::Q;
+        float2* dst = reinterpret_cast<float2*>(halo + p * C::CS + 4 * q);
+        dst[0] = make_float2(v[r][0], v[r][1]);
+        dst[1] = make_float2(v[r][2], v[r][3]);
+      }
+    }
   }
   // ---- 2. weights of tap 0 -> LDS buffer 0; later taps are prefetched through registers
   f32x4 wr[C::WPF];
@@ -162,7 +177,7 @@ void pick_tile(int H, int W, int np, int* pix, int* tw) {
   double best = 1e30;
   for (int P : {256, 128}) {
     if (np == 32 && P == 128) continue;   // 4-wave blocks: keep 256-pixel tiles
-    for (int t : {8, 16, 32, 64}) {
+    for (int t : {8, 16, 32}) {   // TW = 64 would need a larger halo buffer (occupancy)
       const int th = P / t;
       if (th < 2) continue;
       const double cover = (double)((H + th - 1) / th) * th * ((W + t - 1) / t) * t;

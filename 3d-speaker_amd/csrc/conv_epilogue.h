@@ -72,6 +72,56 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
   const bool vec = (d.N % 4 == 0) && (d.ldo % 4 == 0) && (!d.res || d.ldr % 4 == 0) &&
                    (!d.affx || (d.ldx % 4 == 0 && d.ldy % 4 == 0)) && (!d.gate || d.gate_ld % 4 == 0) &&
                    (!d.rowbias || d.rowbias_ld % 4 == 0);
+  // Common case (bias / residual / activations / post-affine only): every residual load of
+  // the wave is issued before the first use, so the whole epilogue is one memory round trip.
+  constexpr int NTL = TM * TN;
+  if constexpr (NTL <= 2) {
+    if (vec && !part && !d.affx && !d.gate && !d.rowbias) {
+      const int c4 = (lane & 7) * 4;
+      f32x4 ra4[NTL][4];
+#pragma unroll
+      for (int tile = 0; tile < NTL; ++tile) {
+        const int i = tile / TN, j = tile % TN;
+        const int n = nwave + j * 32 + c4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          ra4[tile][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (d.res && n < d.N) {
+            const int m = max(0, min(rowmap(i * 32 + q * 8 + (lane >> 3)), M - 1));
+            ra4[tile][q] = *reinterpret_cast<const f32x4*>(d.res + (size_t)m * d.ldr + n);
+          }
+        }
+      }
+#pragma unroll
+      for (int tile = 0; tile < NTL; ++tile) {
+        const int i = tile / TN, j = tile % TN;
+        const int n = nwave + j * 32 + c4;
+        if (n >= d.N) continue;
+        f32x4 bias = {0.f, 0.f, 0.f, 0.f}, ps = {1.f, 1.f, 1.f, 1.f}, pt = {0.f, 0.f, 0.f, 0.f};
+        if (d.bias) bias = *reinterpret_cast<const f32x4*>(d.bias + n);
+        if (d.post_scale) {
+          ps = *reinterpret_cast<const f32x4*>(d.post_scale + n);
+          pt = *reinterpret_cast<const f32x4*>(d.post_shift + n);
+        }
+        const float* ct = cw + tile * 1024;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rl = q * 8 + (lane >> 3);
+          const int m = rowmap(i * 32 + rl);
+          if (m < 0 || m >= M) continue;
+          f32x4 o = *reinterpret_cast<const f32x4*>(ct + rl * 32 + c4) + bias + ra4[tile][q];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float x = apply_act(o[e], d.act);
+            if (d.post_scale) x = x * ps[e] + pt[e];
+            o[e] = apply_act(x, d.act2);
+          }
+          *reinterpret_cast<f32x4*>(d.out + (size_t)m * d.ldo + n) = o;
+        }
+      }
+      return;
+    }
+  }
 #pragma unroll 1
   for (int tile = 0; tile < TM * TN; ++tile) {
     {

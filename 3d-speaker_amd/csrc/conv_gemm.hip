@@ -9,7 +9,7 @@
 // (fusion.py:22-28) and the CAM gate, writing into a channel slice of a wider buffer so
 // torch.cat / torch.split never move data.
 //
-// Tiling: 256 threads = 4 waves, block tile BM x BN, K-tile 16 floats, LDS double buffer
+// Tiling: 64*WM*WN threads, block tile BM x BN, K-tile BK floats, LDS double buffer
 // with register staging (one barrier per K-tile).  Each wave owns (BM/WM) x (BN/WN) as
 // 32x32 MFMA tiles.  fp32 MFMA issues at 64 cycles / SIMD, so LDS bandwidth is not the
 // limit: fragments are read as 2 x ds_read_b128 per 8 MFMA k-steps thanks to a k
@@ -256,7 +256,9 @@ Cfg select_cfg(const ConvDesc& d) {
   if (d.N <= 32) return {256, 32, bk, 8, 1};
   if (d.N <= 64) return {256, 64, bk, 4, 2};
   if (M <= 4096) return {64, 128, bk, 1, 4};
-  return {128, 128, bk, 2, 4};
+  // 128x128 at BK=32 still fits two blocks per CU (73.7 KB LDS): half the K-steps, twice
+  // the loads in flight per step -- what the short-K 1x1 convs need
+  return {128, 128, 32, 2, 4};
 }
 
 template <int BM, int BN, int BK, int WM, int WN>

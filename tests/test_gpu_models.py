@@ -59,7 +59,9 @@ def test_batch_independence_eres2netv2():
     with torch.no_grad():
         full = m(x).cpu().numpy()
         single = np.concatenate([m(x[i:i + 1]).cpu().numpy() for i in range(x.shape[0])])
-    assert helpers.rel_err(full, single).max() < 1e-5
+    # different M picks different tiles / K-steps (fp32 summation order): ~1e-5 noise;
+    # cross-talk between utterances would be O(1)
+    assert helpers.rel_err(full, single).max() < 5e-5
 
 
 def test_weight_reload_invalidates_native_handle():
