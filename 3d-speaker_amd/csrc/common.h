@@ -43,6 +43,8 @@ struct ConvDesc {
   int N = 0;                   // output channels written (incl. zero padding columns)
   int K = 0, Kp = 0;           // K = taps0*s0.cin + s1.cin ; Kp = round_up(K, 16)
   const float* w = nullptr;    // [N][Kp]
+  const uint16_t* wh = nullptr;  // the same weights split for the fp16x3 MFMA path: fp16(w)
+  const uint16_t* wl = nullptr;  //   and fp16((w - fp16(w)) * 2^11), both [N][Kp]
   const float* bias = nullptr; // [N] or null
   const float* rowbias = nullptr; int rowbias_ld = 0;  // per-image bias [nimg][rowbias_ld] (ECAPA ASP context)
   float* out = nullptr; int ldo = 0;

@@ -16,6 +16,8 @@
 // tap (same split for A and B), read as ds_read_b64 pairs.  LDS rows are CIN+2 floats:
 // an odd number of 8-byte slots, so 32 lanes on 32 different pixels (or weight rows) hit
 // distinct banks.
+#include <algorithm>
+
 #include "common.h"
 #include "conv_epilogue.h"
 
@@ -160,6 +162,171 @@ conv3x3_halo_kernel(const ConvDesc d, int TW) {
   });
 }
 
+// Persistent variant for <= 32 output channels (ERes2NetV2 / ERes2Net-large stage 1,
+// CAM++ FCM): all nine taps of the weights stay resident in LDS for the life of the block,
+// and the next tile's input halo is loaded into registers while the MFMAs of the current
+// tile run, so HBM latency is hidden behind compute instead of being paid once per tile.
+// Grid = min(tiles, 2 x CUs); tiles are dealt round-robin (block-uniform trip count).
+template <int CIN, bool ADD>
+struct PersistCfg {
+  static constexpr int NP = 32, PIX = 256, NW = 8, NT = 512;
+  static constexpr int CS = CIN + 2, HC = CIN / 2, Q = CIN / 4;
+  static constexpr int HALO_PIX = 340;                              // (TH+2)(TW+2), TW in {8, 16, 32}
+  static constexpr int HALO = HALO_PIX * CS;
+  static constexpr int WRES = 9 * NP * CS;
+  static constexpr int EPI = NW * 1024;                             // aliases the halo after the taps
+  static constexpr int LDS = (HALO > EPI ? HALO : EPI) + WRES;
+  static constexpr int PF = (HALO_PIX * Q + NT - 1) / NT;           // prefetch float4 per thread
+};
+
+template <int CIN, int TW, bool ADD>
+__global__ void __launch_bounds__(512, 2)
+conv3x3_halo_persistent_kernel(const ConvDesc d) {
+  using C = PersistCfg<CIN, ADD>;
+  __shared__ __attribute__((aligned(16))) float lds[C::LDS];
+  float* halo = lds;
+  float* wres = lds + (C::HALO > C::EPI ? C::HALO : C::EPI);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  constexpr int TH = C::PIX / TW, HW = TW + 2, HH = TH + 2;   // compile-time: no integer divides
+  constexpr int hq = HH * HW * C::Q;
+  const int H = d.Ho, W = d.Wo;
+  const int ntx = (W + TW - 1) / TW, nty = (H + TH - 1) / TH;
+  const int ntiles = d.nimg * ntx * nty;
+
+  f32x4 pa[C::PF], pb[ADD ? C::PF : 1];
+  // tile t's halo (or, with which = 1, its Res2Net addend) -> registers
+  auto pf_load = [&](int t, int which) {
+    const int img = t / (ntx * nty), ty = (t / ntx) % nty, tx = t % ntx;
+    const int y0 = ty * TH - 1, x0 = tx * TW - 1;
+    const float* src = which ? d.s0.p2 : d.s0.p;
+    const int ld = which ? d.s0.ld2 : d.s0.ld;
+#pragma unroll
+    for (int r = 0; r < C::PF; ++r) {
+      const int idx = tid + C::NT * r;
+      const int q = idx % C::Q, p = idx / C::Q;
+      const int gy = y0 + p / HW, gx = x0 + p % HW;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (idx < hq && gy >= 0 && gy < H && gx >= 0 && gx < W)
+        v = *reinterpret_cast<const f32x4*>(src + ((size_t)(img * H + gy) * W + gx) * ld + 4 * q);
+      if (which) pb[r] = v;
+      else pa[r] = v;
+    }
+  };
+  auto pf_store = [&]() {
+#pragma unroll
+    for (int r = 0; r < C::PF; ++r) {
+      const int idx = tid + C::NT * r;
+      if (idx < hq) {
+        f32x4 v = pa[r];
+        if (ADD) v += pb[r];
+        const int q = idx % C::Q, p = idx / C::Q;
+        float2* dst = reinterpret_cast<float2*>(halo + p * C::CS + 4 * q);
+        dst[0] = make_float2(v[0], v[1]);
+        dst[1] = make_float2(v[2], v[3]);
+      }
+    }
+  };
+
+  int t = blockIdx.x;
+  if (t < ntiles) {
+    pf_load(t, 0);
+    if (ADD) pf_load(t, 1);
+  }
+  // all nine taps of the weights -> LDS ([tap][n][CS]); rows n >= N are zero
+  for (int idx = tid; idx < 9 * C::NP * C::Q; idx += C::NT) {
+    const int q = idx % C::Q, n = (idx / C::Q) % C::NP, tap = idx / (C::Q * C::NP);
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (n < d.N) v = *reinterpret_cast<const f32x4*>(d.w + (size_t)n * d.Kp + tap * CIN + 4 * q);
+    float2* dst = reinterpret_cast<float2*>(wres + (tap * C::NP + n) * C::CS + 4 * q);
+    dst[0] = make_float2(v[0], v[1]);
+    dst[1] = make_float2(v[2], v[3]);
+  }
+  if (t < ntiles) pf_store();
+  __syncthreads();
+
+  const int p_own = wave * 32 + li;                 // this lane's A row (pixel of the tile)
+  const int abase = ((p_own / TW) * HW + (p_own % TW)) * C::CS + lh * C::HC;
+  const int bbase = li * C::CS + lh * C::HC;
+  for (; t < ntiles; t += gridDim.x) {
+    const int tn = t + gridDim.x;
+    if (tn < ntiles) pf_load(tn, 0);                // in flight during the taps below
+    f32x16 acc[1][1];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[0][0][r] = 0.f;
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      const float* a = halo + abase + ((tap / 3) * HW + (tap % 3)) * C::CS;
+      const float* b = wres + tap * C::NP * C::CS + bbase;
+#pragma unroll
+      for (int s2 = 0; s2 < C::HC / 2; ++s2) {
+        const float2 av = *reinterpret_cast<const float2*>(a + 2 * s2);
+        const float2 bv = *reinterpret_cast<const float2*>(b + 2 * s2);
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc[0][0], 0, 0, 0);
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc[0][0], 0, 0, 0);
+      }
+    }
+    if (ADD && tn < ntiles) pf_load(tn, 1);         // the addend: in flight during the epilogue
+    __syncthreads();                                // halo reads done: the epilogue reuses it
+    {
+      const int img = t / (ntx * nty), ty = (t / ntx) % nty, tx = t % ntx;
+      const int y0 = ty * TH, x0 = tx * TW;
+      epilogue_tiles<1, 1, true>(d, lds, acc, wave, lane, 0, d.nimg * H * W, [&](int r) {
+        const int p = wave * 32 + r;
+        const int gy = y0 + p / TW, gx = x0 + p % TW;
+        return (gy < H && gx < W) ? (img * H + gy) * W + gx : -1;
+      });
+    }
+    __syncthreads();                                // epilogue LDS reads done
+    if (tn < ntiles) pf_store();
+    __syncthreads();
+  }
+}
+
+int device_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+// resident blocks per CU of a kernel (persistent grids must not exceed what is co-resident)
+template <class K>
+int resident_blocks(K kernel, int threads) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, threads, 0) != hipSuccess || n <= 0) n = 1;
+  return n;
+}
+
+template <int CIN, int TW>
+hipError_t launch_halo_persistent_tw(const ConvDesc& d, hipStream_t s) {
+  constexpr int TH = 256 / TW;
+  const int tiles = d.nimg * ((d.Ho + TH - 1) / TH) * ((d.Wo + TW - 1) / TW);
+  if (d.s0.p2) {
+    auto k = conv3x3_halo_persistent_kernel<CIN, TW, true>;
+    static const int per_cu = resident_blocks(k, 512);
+    hipLaunchKernelGGL(k, dim3(std::min(tiles, per_cu * device_cus())), dim3(512), 0, s, d);
+  } else {
+    auto k = conv3x3_halo_persistent_kernel<CIN, TW, false>;
+    static const int per_cu = resident_blocks(k, 512);
+    hipLaunchKernelGGL(k, dim3(std::min(tiles, per_cu * device_cus())), dim3(512), 0, s, d);
+  }
+  return hipGetLastError();
+}
+
+template <int CIN>
+hipError_t launch_halo_persistent(const ConvDesc& d, int TW, hipStream_t s) {
+  if (TW == 8) return launch_halo_persistent_tw<CIN, 8>(d, s);
+  if (TW == 16) return launch_halo_persistent_tw<CIN, 16>(d, s);
+  return launch_halo_persistent_tw<CIN, 32>(d, s);
+}
+
 template <int CIN, int NP, int PIX>
 hipError_t launch_halo_t(const ConvDesc& d, int TW, hipStream_t s) {
   using C = HaloCfg<CIN, NP, PIX, false>;
@@ -189,6 +356,12 @@ void pick_tile(int H, int W, int np, int* pix, int* tw) {
 
 }  // namespace
 
+// the persistent kernel: <= 32 output channels and the lean epilogue (conv_epilogue.h)
+bool persistent_ok(const ConvDesc& d) {
+  return d.N <= 32 && (d.s0.cin == 28 || d.s0.cin == 32) && d.N % 4 == 0 && d.ldo % 4 == 0 &&
+         (!d.res || d.ldr % 4 == 0) && !d.affx && !d.gate && !d.rowbias && d.ksplit == 1;
+}
+
 bool halo_conv_supported(const ConvDesc& d) {
   const ConvSrc& s = d.s0;
   return s.kh == 3 && s.kw == 3 && s.sh == 1 && s.sw == 1 && s.ph == 1 && s.pw == 1 && s.dh == 1 && s.dw == 1 &&
@@ -202,6 +375,9 @@ std::string halo_kernel_name(const ConvDesc& d) {
   int pix = 256, tw = 16;
   pick_tile(d.Ho, d.Wo, np, &pix, &tw);
   const bool add = d.s0.p2 != nullptr || d.s0.ld2 > 0;
+  if (persistent_ok(d))
+    return "conv3x3_halo_persistent_kernel<" + std::to_string(d.s0.cin) + ", " + std::to_string(tw) + ", " +
+           (add ? "true" : "false") + ">";
   return "conv3x3_halo_kernel<" + std::to_string(d.s0.cin) + ", " + std::to_string(np) + ", " + std::to_string(pix) +
          ", " + (add ? "true" : "false") + ">";
 }
@@ -216,6 +392,8 @@ hipError_t launch_conv3x3_halo(const ConvDesc& d, hipStream_t s) {
     if (np == 32) return launch_halo_t<CI, 32, 256>(d, tw, s);                          \
     return pix == 256 ? launch_halo_t<CI, 64, 256>(d, tw, s) : launch_halo_t<CI, 64, 128>(d, tw, s); \
   }
+  if (persistent_ok(d) && d.s0.cin == 28) return launch_halo_persistent<28>(d, tw, s);
+  if (persistent_ok(d) && d.s0.cin == 32) return launch_halo_persistent<32>(d, tw, s);
   SPK_HALO_CASE(28)
   SPK_HALO_CASE(32)
   SPK_HALO_CASE(52)

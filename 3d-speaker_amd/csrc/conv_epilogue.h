@@ -49,7 +49,9 @@ __device__ __forceinline__ float epilogue_elem(const ConvDesc& d, int m, int n, 
 // layout).  `lds` must have TM*TN*1024 floats per wave free (all waves synchronised before
 // the call); `nwave` is the first output column of the wave; rowmap(r) gives the output
 // row m of the wave's local row r (0 .. 32*TM-1), or -1 when it is outside the output.
-template <int TM, int TN, class RowMap>
+// LEAN = true compiles only the common-case path (bias / residual / act / post-affine,
+// float4-aligned, no split-K); the caller guarantees those conditions on the host.
+template <int TM, int TN, bool LEAN = false, class RowMap>
 __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f32x16 (&acc)[TM][TN], int wave,
                                                int lane, int nwave, int M, RowMap rowmap) {
   const int li = lane & 31, lh = lane >> 5;
@@ -76,7 +78,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
   // the wave is issued before the first use, so the whole epilogue is one memory round trip.
   constexpr int NTL = TM * TN;
   if constexpr (NTL <= 2) {
-    if (vec && !part && !d.affx && !d.gate && !d.rowbias) {
+    if (LEAN || (vec && !part && !d.affx && !d.gate && !d.rowbias)) {
       const int c4 = (lane & 7) * 4;
       f32x4 ra4[NTL][4];
 #pragma unroll
@@ -122,6 +124,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
       return;
     }
   }
+  if constexpr (LEAN) return;
 #pragma unroll 1
   for (int tile = 0; tile < TM * TN; ++tile) {
     {

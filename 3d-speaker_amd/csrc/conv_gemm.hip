@@ -15,10 +15,12 @@
 // limit: fragments are read as 2 x ds_read_b128 per 8 MFMA k-steps thanks to a k
 // permutation (lane half h owns k = 8h + s of the 16-deep tile, identically for A and B).
 // LDS rows are padded to 20 floats, which makes those b128 reads bank-conflict free.
+#include <cstdlib>
 #include <string>
 
 #include "common.h"
 #include "conv_epilogue.h"
+#include "conv_loader.h"
 
 namespace spk {
 
@@ -35,7 +37,7 @@ __device__ __forceinline__ int xcd_remap(int orig, int nblk) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
-template <int BM, int BN, int BK, int WM, int WN, bool S1, bool ADD>
+template <int BM, int BN, int BK, int WM, int WN, bool S1, bool ADD, bool PRE>
 __global__ void __launch_bounds__(64 * WM * WN, 4)
 conv_gemm_kernel(const ConvDesc d) {
   constexpr int NT = 64 * WM * WN;               // threads
@@ -73,103 +75,26 @@ conv_gemm_kernel(const ConvDesc d) {
   const int kt0 = blockIdx.z * per;
   const int kt1 = min(nkt_all, kt0 + per);
 
-  // ---- per-thread A-row geometry (fixed across the K loop)
+  // ---- A: asynchronous implicit-im2col loader (conv_loader.h); B rows clamped + masked
   const int kq = tid % QPR, row0 = tid / QPR;
-  int a_img[AROWS], a_hb[AROWS], a_wb[AROWS], a_h1[AROWS], a_w1[AROWS];
-  bool a_ok[AROWS];
-#pragma unroll
-  for (int r = 0; r < AROWS; ++r) {
-    const int m = m0 + row0 + RPP * r;
-    a_ok[r] = m < M;
-    const int mm = a_ok[r] ? m : 0;
-    const int wo = mm % d.Wo;
-    const int t2 = mm / d.Wo;
-    const int ho = t2 % d.Ho;
-    a_img[r] = t2 / d.Ho;
-    a_hb[r] = ho * d.s0.sh - d.s0.ph;
-    a_wb[r] = wo * d.s0.sw - d.s0.pw;
-    if (S1) { a_h1[r] = ho * d.s1.sh; a_w1[r] = wo * d.s1.sw; }
-  }
-  const int K0 = d.s0.kh * d.s0.kw * d.s0.cin;
-
-  // incremental (tap, channel) decomposition of this thread's k = kt*BK + kq*4
-  int k_c = 0, k_ky = 0, k_kx = 0;
-  {
-    const int k = kt0 * BK + kq * 4;
-    if (k < K0) {
-      const int tap = k / d.s0.cin;
-      k_c = k - tap * d.s0.cin;
-      k_ky = tap / d.s0.kw;
-      k_kx = tap - k_ky * d.s0.kw;
-    } else {
-      k_ky = d.s0.kh; k_c = k - K0;   // in s1 (or beyond K)
-    }
-  }
-
-  f32x4 ra[AROWS], rb[BROWS];
+  using AL = ALoader<AROWS, RPP, BK, S1, ADD, PRE>;
+  AL al;
+  al.init(d, m0, row0, kq, kt0);
+  typename AL::Slot sa;
+  f32x4 rb[BROWS];
+  unsigned bok = 0;
 
   auto load_tile = [&](int kt) {
+    al.load(d, sa);
     const int k = kt * BK + kq * 4;
-    // ---- A (implicit im2col; zero outside the image / beyond K)
-    if (k_ky < d.s0.kh) {
-      const bool pre = d.s0.pre_scale != nullptr;
-      f32x4 psc = {1.f, 1.f, 1.f, 1.f}, psh = {0.f, 0.f, 0.f, 0.f};
-      if (pre) {
-        psc = *reinterpret_cast<const f32x4*>(d.s0.pre_scale + k_c);
-        psh = *reinterpret_cast<const f32x4*>(d.s0.pre_shift + k_c);
-      }
-#pragma unroll
-      for (int r = 0; r < AROWS; ++r) {
-        int hi = a_hb[r] + k_ky * d.s0.dh;
-        int wi = a_wb[r] + k_kx * d.s0.dw;
-        if (d.s0.reflect) {
-          hi = hi < 0 ? -hi : (hi >= d.s0.H ? 2 * d.s0.H - 2 - hi : hi);
-          wi = wi < 0 ? -wi : (wi >= d.s0.W ? 2 * d.s0.W - 2 - wi : wi);
-        }
-        const bool ok = a_ok[r] && hi >= 0 && hi < d.s0.H && wi >= 0 && wi < d.s0.W;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (ok) {
-          const size_t pix = (size_t)(a_img[r] * d.s0.H + hi) * d.s0.W + wi;
-          v = *reinterpret_cast<const f32x4*>(d.s0.p + pix * d.s0.ld + k_c);
-          if (ADD) v += *reinterpret_cast<const f32x4*>(d.s0.p2 + pix * d.s0.ld2 + k_c);
-          if (pre) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = fmaxf(fmaf(v[q], psc[q], psh[q]), 0.f);
-          }
-        }
-        ra[r] = v;
-      }
-    } else if (S1 && k_c < d.s1.cin) {
-#pragma unroll
-      for (int r = 0; r < AROWS; ++r) {
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (a_ok[r]) {
-          const size_t pix = (size_t)(a_img[r] * d.s1.H + a_h1[r]) * d.s1.W + a_w1[r];
-          v = *reinterpret_cast<const f32x4*>(d.s1.p + pix * d.s1.ld + k_c);
-        }
-        ra[r] = v;
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < AROWS; ++r) ra[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    // advance (tap, c) by BK for the next tile
-    if (k_ky < d.s0.kh) {
-      k_c += BK;
-      while (k_c >= d.s0.cin && k_ky < d.s0.kh) {
-        k_c -= d.s0.cin;
-        if (++k_kx == d.s0.kw) { k_kx = 0; ++k_ky; }
-      }
-    } else {
-      k_c += BK;
-    }
-    // ---- B (packed weights [N][Kp])
+    bok = 0;
 #pragma unroll
     for (int r = 0; r < BROWS; ++r) {
       const int nr = row0 + RPP * r;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (nr < BN && n0 + nr < d.N) v = *reinterpret_cast<const f32x4*>(d.w + (size_t)(n0 + nr) * d.Kp + k);
-      rb[r] = v;
+      const bool ok = nr < BN && n0 + nr < d.N;
+      const int n = ok ? n0 + nr : 0;
+      rb[r] = *reinterpret_cast<const f32x4*>(d.w + (size_t)n * d.Kp + k);
+      if (ok) bok |= 1u << r;
     }
   };
 
@@ -177,11 +102,13 @@ conv_gemm_kernel(const ConvDesc d) {
     float* a = As + buf * BM * LDS_ROW;
     float* b = Bs + buf * BN * LDS_ROW;
 #pragma unroll
-    for (int r = 0; r < AROWS; ++r) *reinterpret_cast<f32x4*>(a + (row0 + RPP * r) * LDS_ROW + kq * 4) = ra[r];
+    for (int r = 0; r < AROWS; ++r)
+      *reinterpret_cast<f32x4*>(a + (row0 + RPP * r) * LDS_ROW + kq * 4) = al.value(sa, r);
 #pragma unroll
     for (int r = 0; r < BROWS; ++r) {
       const int nr = row0 + RPP * r;
-      if (nr < BN) *reinterpret_cast<f32x4*>(b + nr * LDS_ROW + kq * 4) = rb[r];
+      if (nr < BN)
+        *reinterpret_cast<f32x4*>(b + nr * LDS_ROW + kq * 4) = ((bok >> r) & 1) ? rb[r] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
 
@@ -235,6 +162,183 @@ conv_gemm_kernel(const ConvDesc d) {
   epilogue_tiles<TM, TN>(d, lds, acc, wave, lane, n0 + wn * WTN, M, [&](int r) { return m0 + wm * WTM + r; });
 }
 
+// ---------------------------------------------------------------------------------------
+// fp16x3: fp32-accurate GEMM on the fp16 matrix cores (v_mfma_f32_32x32x16_f16, 16x the
+// fp32 MFMA's work per cycle).  Every operand x is split as hi = fp16(x) and
+// lo = fp16((x - hi) * 2^11) (the 2^11 keeps lo out of the fp16 subnormal range), and
+//   x * w  ~=  hi_x * hi_w  +  2^-11 * (hi_x * lo_w + lo_x * hi_w)
+// with products exact and sums in fp32 (two accumulators); the dropped lo*lo term is
+// 2^-22 relative.  Embeddings stay within the reference's own fp32-vs-fp64 noise
+// (DESIGN.md §4).  Weights are split once at model creation (misc.hip split_f16);
+// activations are split while they are staged into LDS, so HBM traffic is unchanged
+// (fp32 in, fp32 out).
+//
+// LDS per buffer: A hi / A lo / B hi / B lo planes, rows of BK = 32 halves padded to 40
+// (80 B: the same conflict-free ds_read_b128 pattern as the fp32 kernel's 20-float rows).
+// Lane half h owns k = 16h .. 16h+15 of the tile: k-step s reads halves 16h + 8s .. +7
+// for both operands (a k permutation shared by A and B, so the products pair up).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int BM, int BN, int WM, int WN>
+struct X3Cfg {
+  static constexpr int BK = 32, NT = 64 * WM * WN;
+  static constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32;
+  static constexpr int QPR = BK / 4, RPP = NT / QPR, AROWS = BM / RPP;             // A: fp32 quads
+  static constexpr int CPR = 8, RPPB = NT / CPR, BROWS = (BN + RPPB - 1) / RPPB;   // B: 16-B chunks
+  static constexpr int LROW = BK + 8;                                               // halves
+  static constexpr int PA = BM * LROW, PB = BN * LROW;
+  static constexpr int STAGE = 2 * PA + 2 * PB;       // halves per buffer = floats for both buffers
+  static constexpr int LDS_EPI = WM * WN * TM * TN * 1024;
+  static constexpr int LDS_FLOATS = STAGE > LDS_EPI ? STAGE : LDS_EPI;
+};
+
+template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE>
+__global__ void __launch_bounds__(64 * WM * WN, 1)
+conv_gemm_x3_kernel(const ConvDesc d) {
+  using C = X3Cfg<BM, BN, WM, WN>;
+  constexpr int BK = C::BK, TM = C::TM, TN = C::TN, RPP = C::RPP, AROWS = C::AROWS;
+  static_assert(TM >= 1 && TN >= 1 && BM % RPP == 0, "tile shape");
+  __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
+  _Float16* hl = reinterpret_cast<_Float16*>(lds);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int M = d.nimg * d.Ho * d.Wo;
+  const int nN = (d.N + BN - 1) / BN;
+  const int nM = (M + BM - 1) / BM;
+  const int lid = xcd_remap(blockIdx.x, nM * nN);
+  const int mt = lid / nN, nt = lid % nN;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const int nkt_all = d.Kp / BK;
+  const int per = (nkt_all + d.ksplit - 1) / d.ksplit;
+  const int kt0 = blockIdx.z * per;
+  const int kt1 = min(nkt_all, kt0 + per);
+
+  // ---- A: asynchronous implicit-im2col loader (conv_loader.h)
+  const int kq = tid % C::QPR, row0 = tid / C::QPR;
+  using AL = ALoader<AROWS, RPP, BK, S1, ADD, PRE>;
+  AL al;
+  al.init(d, m0, row0, kq, kt0);
+  // ---- B chunk geometry: chunk cb = (plane, quarter) of a 32-half weight row
+  const int cb = tid % C::CPR, brow0 = tid / C::CPR;
+  const uint16_t* bsrc = (cb >> 2) ? d.wl : d.wh;
+  const int bq = cb & 3;
+
+  // two register sets: the loads of K-tile kt+2 are issued before the MFMAs of tile kt, so
+  // every load has two K-steps of compute to land (prefetch distance 2, LDS double buffer)
+  struct Set {
+    typename AL::Slot a;
+    u32x4 b[C::BROWS];
+    unsigned bok;
+  };
+  Set set0, set1;
+
+  auto load_tile = [&](int kt, Set& st) {
+    al.load(d, st.a);
+    st.bok = 0;
+#pragma unroll
+    for (int r = 0; r < C::BROWS; ++r) {
+      const int nr = brow0 + C::RPPB * r;
+      const bool ok = nr < BN && n0 + nr < d.N;
+      const int n = ok ? n0 + nr : 0;
+      st.b[r] = *reinterpret_cast<const u32x4*>(bsrc + (size_t)n * d.Kp + kt * BK + bq * 8);
+      if (ok) st.bok |= 1u << r;
+    }
+  };
+
+  auto store_tile = [&](int buf, const Set& st) {
+    _Float16* ahi = hl + buf * C::STAGE;
+    _Float16* alo = ahi + C::PA;
+    _Float16* bpl = ahi + 2 * C::PA + (cb >> 2) * C::PB;
+#pragma unroll
+    for (int r = 0; r < AROWS; ++r) {
+      const f32x4 v = al.value(st.a, r);
+      f16x4 h, l;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const _Float16 x = (_Float16)v[e];
+        h[e] = x;
+        l[e] = (_Float16)((v[e] - (float)x) * 2048.0f);
+      }
+      const int off = (row0 + RPP * r) * C::LROW + kq * 4;
+      *reinterpret_cast<f16x4*>(ahi + off) = h;
+      *reinterpret_cast<f16x4*>(alo + off) = l;
+    }
+#pragma unroll
+    for (int r = 0; r < C::BROWS; ++r) {
+      const int nr = brow0 + C::RPPB * r;
+      if (nr < BN)
+        *reinterpret_cast<u32x4*>(bpl + nr * C::LROW + bq * 8) = ((st.bok >> r) & 1) ? st.b[r] : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+
+  f32x16 acc[TM][TN], accx[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; accx[i][j][r] = 0.f; }
+
+  const int li = lane & 31, lh = lane >> 5;
+  auto compute = [&](int buf) {
+    const _Float16* ahi = hl + buf * C::STAGE;
+    const _Float16* bhi = ahi + 2 * C::PA;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      f16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const _Float16* p = ahi + (wm * C::WTM + i * 32 + li) * C::LROW + lh * 16 + 8 * s;
+        ah[i] = *reinterpret_cast<const f16x8*>(p);
+        al[i] = *reinterpret_cast<const f16x8*>(p + C::PA);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const _Float16* p = bhi + (wn * C::WTN + j * 32 + li) * C::LROW + lh * 16 + 8 * s;
+        bh[j] = *reinterpret_cast<const f16x8*>(p);
+        bl[j] = *reinterpret_cast<const f16x8*>(p + C::PB);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          accx[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], accx[i][j], 0, 0, 0);
+          accx[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], accx[i][j], 0, 0, 0);
+        }
+    }
+  };
+  if (kt0 < kt1) {
+    load_tile(kt0, set0);
+    if (kt0 + 1 < kt1) load_tile(kt0 + 1, set1);
+    store_tile(0, set0);
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; kt += 2) {
+      // even step: LDS buffer 0 holds kt, set 1 holds kt+1 (in flight), set 0 is free
+      if (kt + 2 < kt1) load_tile(kt + 2, set0);
+      compute(0);
+      if (kt + 1 < kt1) store_tile(1, set1);
+      __syncthreads();
+      if (kt + 1 >= kt1) break;
+      // odd step: buffer 1 holds kt+1, set 0 holds kt+2 (in flight), set 1 is free
+      if (kt + 3 < kt1) load_tile(kt + 3, set1);
+      compute(1);
+      if (kt + 2 < kt1) store_tile(0, set0);
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] += accx[i][j] * (1.0f / 2048.0f);
+  epilogue_tiles<TM, TN>(d, lds, acc, wave, lane, n0 + wn * C::WTN, M, [&](int r) { return m0 + wm * C::WTM + r; });
+}
+
 // Split-K combine: out = epi(sum_z partial[z])   (fixed z order: deterministic)
 __global__ void splitk_reduce_kernel(const ConvDesc d, int M) {
   const size_t total = (size_t)M * d.N;
@@ -261,17 +365,32 @@ Cfg select_cfg(const ConvDesc& d) {
   return {128, 128, 32, 2, 4};
 }
 
+// fp16x3 split-precision MFMA (default) or exact fp32 MFMA (SPK_CONV_MFMA=f32)
+bool use_x3() {
+  static const bool x3 = [] {
+    const char* e = std::getenv("SPK_CONV_MFMA");
+    return !(e && std::string(e) == "f32");
+  }();
+  return x3;
+}
+
 template <int BM, int BN, int BK, int WM, int WN>
 hipError_t launch_cfg(const ConvDesc& d, hipStream_t s) {
   const int M = d.nimg * d.Ho * d.Wo;
   const int nblk = ((M + BM - 1) / BM) * ((d.N + BN - 1) / BN);
   dim3 grid(nblk, 1, d.ksplit);
   dim3 block(64 * WM * WN);
-  const bool s1 = d.s1.p != nullptr, add = d.s0.p2 != nullptr;
-  if (s1 && add) return hipErrorInvalidValue;
-  if (s1) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, true, false>), grid, block, 0, s, d);
-  else if (add) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, false, true>), grid, block, 0, s, d);
-  else hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, false, false>), grid, block, 0, s, d);
+  const bool s1 = d.s1.p != nullptr, add = d.s0.p2 != nullptr, pre = d.s0.pre_scale != nullptr;
+  if ((int)s1 + (int)add + (int)pre > 1) return hipErrorInvalidValue;
+  if (use_x3() && d.wh && d.wl) {
+    if (s1) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, true, false, false>), grid, block, 0, s, d);
+    else if (add) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, true, false>), grid, block, 0, s, d);
+    else if (pre) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, false, true>), grid, block, 0, s, d);
+    else hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, false, false>), grid, block, 0, s, d);
+  } else if (s1) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, true, false, false>), grid, block, 0, s, d);
+  else if (add) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, false, true, false>), grid, block, 0, s, d);
+  else if (pre) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, false, false, true>), grid, block, 0, s, d);
+  else hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, false, false, false>), grid, block, 0, s, d);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || d.ksplit <= 1) return e;
   const size_t total = (size_t)M * d.N;
@@ -295,9 +414,13 @@ std::string conv_kernel_name(const ConvDesc& d) {
   if (halo_conv_supported(d)) return halo_kernel_name(d);
   const Cfg c = select_cfg(d);
   const bool s1 = d.s1.p != nullptr || d.s1.cin > 0, add = d.s0.p2 != nullptr || d.s0.ld2 > 0;
+  const bool pre = d.s0.pre_scale != nullptr;
+  const std::string tail = std::to_string(c.wm) + ", " + std::to_string(c.wn) + ", " + (s1 ? "true" : "false") + ", " +
+                           (add ? "true" : "false") + ", " + (pre ? "true" : "false") + ">";
+  if (use_x3() && d.wh && d.wl)
+    return "conv_gemm_x3_kernel<" + std::to_string(c.bm) + ", " + std::to_string(c.bn) + ", " + tail;
   return "conv_gemm_kernel<" + std::to_string(c.bm) + ", " + std::to_string(c.bn) + ", " + std::to_string(c.bk) + ", " +
-         std::to_string(c.wm) + ", " + std::to_string(c.wn) + ", " + (s1 ? "true" : "false") + ", " +
-         (add ? "true" : "false") + ">";
+         tail;
 }
 
 int conv_tile_blocks(const ConvDesc& d) {

@@ -106,4 +106,21 @@ hipError_t launch_tstp(const float* x, int B, int H, int W, int C, int ld, float
   return hipGetLastError();
 }
 
+__global__ void split_f16_kernel(const float* w, _Float16* hi, _Float16* lo, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float v = w[i];
+    const _Float16 h = (_Float16)v;
+    hi[i] = h;
+    lo[i] = (_Float16)((v - (float)h) * 2048.0f);
+  }
+}
+
+hipError_t launch_split_f16(const float* w, uint16_t* hi, uint16_t* lo, size_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const int blocks = (int)std::min<size_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(split_f16_kernel, dim3(blocks), dim3(256), 0, s, w, reinterpret_cast<_Float16*>(hi),
+                     reinterpret_cast<_Float16*>(lo), n);
+  return hipGetLastError();
+}
+
 }  // namespace spk

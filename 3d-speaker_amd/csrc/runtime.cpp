@@ -159,6 +159,8 @@ void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const C
   if (!plan) return;
   d.N = p.N; d.K = p.K; d.Kp = p.Kp;
   d.w = m.dptr(p.w_off);
+  d.wh = m.dhi(p.w_off);
+  d.wl = m.dlo(p.w_off);
   d.bias = (use_bias && p.has_bias) ? m.dptr(p.b_off) : nullptr;
   const int M = d.nimg * d.Ho * d.Wo;
   // split-K for skinny, deep GEMMs (e.g. the 20480 -> 192 embedding layer)
@@ -331,6 +333,18 @@ int spk_model_create(const spk_model_config_t* cfg, const spk_weight_t* weights,
       (void)hipFree(h->m.dweights);
       return rc;
     }
+    {
+      // fp16 hi / lo planes of every packed weight for the fp16x3 GEMM (split on the device)
+      const size_t n = h->m.dweights_bytes / sizeof(float);
+      if (int rc = hip_check(hipMalloc(&h->m.dsplit, std::max<size_t>(2 * n * sizeof(uint16_t), 256)),
+                             "hipMalloc(split weights)")) {
+        (void)hipFree(h->m.dweights);
+        return rc;
+      }
+      if (int rc = hip_check(launch_split_f16(h->m.dweights, h->m.dsplit, h->m.dsplit + n, n, nullptr), "split_f16"))
+        return rc;
+      if (int rc = hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize")) return rc;
+    }
     h->m.uploaded = true;
     h->m.arena.clear();
     h->m.arena.shrink_to_fit();
@@ -343,6 +357,7 @@ int spk_model_create(const spk_model_config_t* cfg, const spk_weight_t* weights,
 int spk_model_destroy(spk_model_t* model) {
   if (!model) return SPK_OK;
   if (model->m.dweights) (void)hipFree(model->m.dweights);
+  if (model->m.dsplit) (void)hipFree(model->m.dsplit);
   delete model;
   return SPK_OK;
 }

@@ -92,6 +92,7 @@ struct Model {
   std::vector<float> arena;                       // packed host weights (dropped after upload)
   float* dweights = nullptr;
   size_t dweights_bytes = 0;
+  uint16_t* dsplit = nullptr;                     // fp16 hi plane then lo plane of the whole arena
   std::map<std::string, Packed> packed;
   std::map<std::pair<int, int>, std::unique_ptr<Plan>> plans;
   std::mutex mu;
@@ -105,6 +106,8 @@ struct Model {
 
   size_t put(const std::vector<float>& v);        // append 64-float aligned, return offset (floats)
   const float* dptr(size_t off) const { return dweights + off; }
+  const uint16_t* dhi(size_t off) const { return dsplit ? dsplit + off : nullptr; }
+  const uint16_t* dlo(size_t off) const { return dsplit ? dsplit + dweights_bytes / sizeof(float) + off : nullptr; }
   // fold BN (+conv bias) into per-output-channel (scale, shift) in double precision
   void bn_fold(const std::string& bn, int n, std::vector<double>& s, std::vector<double>& t, double eps = 1e-5) const;
   const Packed& pack(const std::string& name, const ChanMap& out, const std::vector<Part>& parts, int K);

@@ -92,6 +92,9 @@ hipError_t launch_conv(const ConvDesc& d, hipStream_t) {
 
 std::string conv_kernel_name(const ConvDesc&) { return "emu_conv"; }
 
+// the emulated GEMM reads the fp32 weights; the split planes are not needed on the host
+hipError_t launch_split_f16(const float*, uint16_t*, uint16_t*, size_t, hipStream_t) { return hipSuccess; }
+
 hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const float* w, const float* bias, int cout,
                                int act, int wstride, float* out, int ldo, hipStream_t) {
   for (int b = 0; b < B; ++b)
@@ -157,6 +160,7 @@ hipError_t launch_cosine_affinity(const float* A, long long Na, const float* B, 
 extern "C" {
 hipError_t hipMalloc(void** p, size_t n) { *p = std::malloc(n ? n : 1); return *p ? hipSuccess : hipErrorOutOfMemory; }
 hipError_t hipFree(void* p) { std::free(p); return hipSuccess; }
+hipError_t hipDeviceSynchronize(void) { return hipSuccess; }
 hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind) { std::memcpy(d, s, n); return hipSuccess; }
 hipError_t hipGetDevice(int* d) { *d = 0; return hipSuccess; }
 hipError_t hipGetLastError(void) { return hipSuccess; }

@@ -15,3 +15,9 @@ for a in $arch ${2:-}; do
   if [ $rc -ne 0 ]; then exit $rc; fi
   python tools/agg_steps.py gpurun_out/steps_$a.json | head -24
 done
+if [ -n "${CMP_F32:-}" ]; then
+  echo "== steps $arch fp32-MFMA $(date +%T)"
+  SPK_CONV_MFMA=f32 timeout -k 10 300 python tools/profile_steps.py --arch $arch --json gpurun_out/steps_${arch}_f32.json > gpurun_out/steps_${arch}_f32.txt 2>&1
+  grep -v amdgpu.ids gpurun_out/steps_${arch}_f32.txt | head -2
+  python tools/agg_steps.py gpurun_out/steps_${arch}_f32.json | head -16
+fi
