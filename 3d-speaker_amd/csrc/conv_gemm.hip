@@ -350,6 +350,26 @@ __global__ void splitk_reduce_kernel(const ConvDesc d, int M) {
   }
 }
 
+// fp16x3 split-precision MFMA (default) or exact fp32 MFMA (SPK_CONV_MFMA=f32)
+bool use_x3() {
+  static const bool x3 = [] {
+    const char* e = std::getenv("SPK_CONV_MFMA");
+    return !(e && std::string(e) == "f32");
+  }();
+  return x3;
+}
+
+// x3 tile override for experiments: SPK_X3_TILE=128x128 | 256x128 | 128x256
+int x3_tile() {
+  static const int t = [] {
+    const char* e = std::getenv("SPK_X3_TILE");
+    if (!e) return 0;
+    const std::string v(e);
+    return v == "256x128" ? 1 : v == "128x256" ? 2 : v == "128x128" ? 3 : 0;
+  }();
+  return t;
+}
+
 struct Cfg {
   int bm, bn, bk, wm, wn;
 };
@@ -360,18 +380,18 @@ Cfg select_cfg(const ConvDesc& d) {
   if (d.N <= 32) return {256, 32, bk, 8, 1};
   if (d.N <= 64) return {256, 64, bk, 4, 2};
   if (M <= 4096) return {64, 128, bk, 1, 4};
+  if (use_x3() && d.wh) {
+    const int t = x3_tile();
+    if (t == 1) return {256, 128, 32, 4, 2};
+    if (t == 2) return {128, 256, 32, 2, 4};
+    if (t == 3) return {128, 128, 32, 2, 4};
+    // deep K: bigger tiles halve the L2 traffic per FLOP (measured per layer)
+    if (d.Kp >= 1024 && d.N >= 512 && d.N % 256 == 0) return {128, 256, 32, 2, 4};
+    if (d.Kp >= 256) return {256, 128, 32, 4, 2};
+  }
   // 128x128 at BK=32 still fits two blocks per CU (73.7 KB LDS): half the K-steps, twice
   // the loads in flight per step -- what the short-K 1x1 convs need
   return {128, 128, 32, 2, 4};
-}
-
-// fp16x3 split-precision MFMA (default) or exact fp32 MFMA (SPK_CONV_MFMA=f32)
-bool use_x3() {
-  static const bool x3 = [] {
-    const char* e = std::getenv("SPK_CONV_MFMA");
-    return !(e && std::string(e) == "f32");
-  }();
-  return x3;
 }
 
 template <int BM, int BN, int BK, int WM, int WN>
@@ -404,6 +424,8 @@ hipError_t launch_bk(const ConvDesc& d, const Cfg& c, hipStream_t s) {
   if (c.bn == 32) return launch_cfg<256, 32, BK, 8, 1>(d, s);
   if (c.bn == 64) return launch_cfg<256, 64, BK, 4, 2>(d, s);
   if (c.bm == 64) return launch_cfg<64, 128, BK, 1, 4>(d, s);
+  if (c.bm == 256) return launch_cfg<256, 128, BK, 4, 2>(d, s);
+  if (c.bn == 256) return launch_cfg<128, 256, BK, 2, 4>(d, s);
   return launch_cfg<128, 128, BK, 2, 4>(d, s);
 }
 
