@@ -61,12 +61,17 @@ struct ConvDesc {
 };
 
 hipError_t launch_conv(const ConvDesc& d, hipStream_t s);
+bool conv_use_x3();   // fp16x3 split-precision MFMA path (default; SPK_CONV_MFMA=f32 selects exact fp32 MFMA)
 std::string conv_kernel_name(const ConvDesc& d);
 int conv_tile_blocks(const ConvDesc& d);
 // halo-tiled 3x3 kernel for small channel counts (conv3x3_halo.hip); launch_conv routes to it
 bool halo_conv_supported(const ConvDesc& d);
 hipError_t launch_conv3x3_halo(const ConvDesc& d, hipStream_t s);
-std::string halo_kernel_name(const ConvDesc& d);   // blocks of one split of the tile config launch_conv picks
+std::string halo_kernel_name(const ConvDesc& d);
+// persistent short-K 1x1 GEMM (pw_gemm.hip); launch_conv routes to it
+bool pw_supported(const ConvDesc& d);
+hipError_t launch_pw(const ConvDesc& d, hipStream_t s);
+std::string pw_kernel_name(const ConvDesc& d);   // blocks of one split of the tile config launch_conv picks
 
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 

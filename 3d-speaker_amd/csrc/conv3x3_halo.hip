@@ -17,6 +17,7 @@
 // an odd number of 8-byte slots, so 32 lanes on 32 different pixels (or weight rows) hit
 // distinct banks.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "conv_epilogue.h"
@@ -284,6 +285,143 @@ conv3x3_halo_persistent_kernel(const ConvDesc d) {
   }
 }
 
+// fp16x3 variant of the persistent kernel (conv_gemm.hip "fp16x3"): the halo and the
+// resident weights are held as fp16 hi / lo planes, channels padded to CINP = 32 (one or two
+// 16-deep k-steps per tap), pixel rows of CINP + 8 halves (conflict-free ds_read_b128).
+// The halo loads are unconditional (clamped address, zero applied from a mask at staging)
+// so they stay in flight across the taps.
+template <int CIN>
+struct HaloX3Cfg {
+  static constexpr int NP = 32, PIX = 256, NW = 8, NT = 512;
+  static constexpr int CINP = 32, ROW = CINP + 8, QP = CINP / 4, Q = CIN / 4;
+  static constexpr int HALO_PIX = 340;                              // (TH+2)(TW+2), TW in {8, 16, 32}
+  static constexpr int HALO_F = HALO_PIX * ROW;                     // floats = hi + lo halves
+  static constexpr int WRES_F = 9 * NP * ROW;                       // floats = hi + lo halves
+  static constexpr int EPI = NW * 1024;
+  static constexpr int LDS = (HALO_F > EPI ? HALO_F : EPI) + WRES_F;
+  static constexpr int PF = (HALO_PIX * QP + NT - 1) / NT;          // staged float4 per thread
+};
+
+template <int CIN, int TW, bool ADD>
+__global__ void __launch_bounds__(512, 1)
+conv3x3_halo_x3_kernel(const ConvDesc d) {
+  using C = HaloX3Cfg<CIN>;
+  typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+  typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) float lds[C::LDS];
+  _Float16* hh = reinterpret_cast<_Float16*>(lds);                 // halo hi plane
+  _Float16* hlo = hh + C::HALO_PIX * C::ROW;                        // halo lo plane
+  _Float16* wh = reinterpret_cast<_Float16*>(lds + (C::HALO_F > C::EPI ? C::HALO_F : C::EPI));
+  _Float16* wl = wh + 9 * C::NP * C::ROW;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  constexpr int TH = C::PIX / TW, HW = TW + 2, HH = TH + 2;
+  constexpr int hq = HH * HW * C::QP;
+  const int H = d.Ho, W = d.Wo;
+  const int ntx = (W + TW - 1) / TW, nty = (H + TH - 1) / TH;
+  const int ntiles = d.nimg * ntx * nty;
+
+  f32x4 pa[C::PF], pb[ADD ? C::PF : 1];
+  unsigned pok = 0;
+  auto pf_load = [&](int t) {
+    const int img = t / (ntx * nty), ty = (t / ntx) % nty, tx = t % ntx;
+    const int y0 = ty * TH - 1, x0 = tx * TW - 1;
+    pok = 0;
+#pragma unroll
+    for (int r = 0; r < C::PF; ++r) {
+      const int idx = tid + C::NT * r;
+      const int q = idx % C::QP, p = idx / C::QP;
+      const int gy = y0 + p / HW, gx = x0 + p % HW;
+      const bool ok = idx < hq && q < C::Q && gy >= 0 && gy < H && gx >= 0 && gx < W;
+      const size_t pix = ok ? (size_t)(img * H + gy) * W + gx : 0;
+      const int c = ok ? 4 * q : 0;
+      pa[r] = *reinterpret_cast<const f32x4*>(d.s0.p + pix * d.s0.ld + c);
+      if (ADD) pb[r] = *reinterpret_cast<const f32x4*>(d.s0.p2 + pix * d.s0.ld2 + c);
+      pok |= ok ? 1u << r : 0u;
+    }
+  };
+  auto pf_store = [&]() {
+#pragma unroll
+    for (int r = 0; r < C::PF; ++r) {
+      const int idx = tid + C::NT * r;
+      if (idx < hq) {
+        f32x4 v = pa[r];
+        if (ADD) v += pb[r];
+        if (!((pok >> r) & 1)) v = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int q = idx % C::QP, p = idx / C::QP;
+        f16x4 h, l;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const _Float16 x = (_Float16)v[e];
+          h[e] = x;
+          l[e] = (_Float16)((v[e] - (float)x) * 2048.0f);
+        }
+        *reinterpret_cast<f16x4*>(hh + p * C::ROW + 4 * q) = h;
+        *reinterpret_cast<f16x4*>(hlo + p * C::ROW + 4 * q) = l;
+      }
+    }
+  };
+
+  int t = blockIdx.x;
+  if (t < ntiles) pf_load(t);
+  // all nine taps of the split weights -> LDS ([tap][n][ROW] hi / lo); channels >= CIN zero
+  for (int idx = tid; idx < 9 * C::NP * C::QP; idx += C::NT) {
+    const int q = idx % C::QP, n = (idx / C::QP) % C::NP, tap = idx / (C::QP * C::NP);
+    typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+    u16x4 h = {0, 0, 0, 0}, l = {0, 0, 0, 0};
+    if (n < d.N && q < C::Q) {
+      const size_t o = (size_t)n * d.Kp + tap * CIN + 4 * q;
+      h = *reinterpret_cast<const u16x4*>(d.wh + o);
+      l = *reinterpret_cast<const u16x4*>(d.wl + o);
+    }
+    *reinterpret_cast<u16x4*>(wh + (tap * C::NP + n) * C::ROW + 4 * q) = h;
+    *reinterpret_cast<u16x4*>(wl + (tap * C::NP + n) * C::ROW + 4 * q) = l;
+  }
+  if (t < ntiles) pf_store();
+  __syncthreads();
+
+  const int p_own = wave * 32 + li;
+  const int abase = ((p_own / TW) * HW + (p_own % TW)) * C::ROW + 8 * lh;
+  const int bbase = li * C::ROW + 8 * lh;
+  for (; t < ntiles; t += gridDim.x) {
+    const int tn = t + gridDim.x;
+    if (tn < ntiles) pf_load(tn);                   // in flight during the taps and epilogue
+    f32x16 acc[1][1], accx;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { acc[0][0][r] = 0.f; accx[r] = 0.f; }
+#pragma unroll 3
+    for (int tap = 0; tap < 9; ++tap) {
+      const int aoff = abase + ((tap / 3) * HW + (tap % 3)) * C::ROW;
+      const int boff = tap * C::NP * C::ROW + bbase;
+#pragma unroll
+      for (int s = 0; s < C::CINP / 16; ++s) {
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(hh + aoff + 16 * s);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(hlo + aoff + 16 * s);
+        const f16x8 bh = *reinterpret_cast<const f16x8*>(wh + boff + 16 * s);
+        const f16x8 bl = *reinterpret_cast<const f16x8*>(wl + boff + 16 * s);
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[0][0], 0, 0, 0);
+        accx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, accx, 0, 0, 0);
+        accx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, accx, 0, 0, 0);
+      }
+    }
+    acc[0][0] += accx * (1.0f / 2048.0f);
+    __syncthreads();                                // halo reads done: the epilogue reuses it
+    {
+      const int img = t / (ntx * nty), ty = (t / ntx) % nty, tx = t % ntx;
+      const int y0 = ty * TH, x0 = tx * TW;
+      epilogue_tiles<1, 1, true>(d, lds, acc, wave, lane, 0, d.nimg * H * W, [&](int r) {
+        const int p = wave * 32 + r;
+        const int gy = y0 + p / TW, gx = x0 + p % TW;
+        return (gy < H && gx < W) ? (img * H + gy) * W + gx : -1;
+      });
+    }
+    __syncthreads();                                // epilogue LDS reads done
+    if (tn < ntiles) pf_store();
+    __syncthreads();
+  }
+}
+
 int device_cus() {
   static int cached[64] = {0};
   int dev = 0;
@@ -308,6 +446,18 @@ template <int CIN, int TW>
 hipError_t launch_halo_persistent_tw(const ConvDesc& d, hipStream_t s) {
   constexpr int TH = 256 / TW;
   const int tiles = d.nimg * ((d.Ho + TH - 1) / TH) * ((d.Wo + TW - 1) / TW);
+  if (conv_use_x3() && d.wh && d.wl) {
+    if (d.s0.p2) {
+      auto k = conv3x3_halo_x3_kernel<CIN, TW, true>;
+      static const int per_cu = resident_blocks(k, 512);
+      hipLaunchKernelGGL(k, dim3(std::min(tiles, per_cu * device_cus())), dim3(512), 0, s, d);
+    } else {
+      auto k = conv3x3_halo_x3_kernel<CIN, TW, false>;
+      static const int per_cu = resident_blocks(k, 512);
+      hipLaunchKernelGGL(k, dim3(std::min(tiles, per_cu * device_cus())), dim3(512), 0, s, d);
+    }
+    return hipGetLastError();
+  }
   if (d.s0.p2) {
     auto k = conv3x3_halo_persistent_kernel<CIN, TW, true>;
     static const int per_cu = resident_blocks(k, 512);
@@ -363,7 +513,12 @@ bool persistent_ok(const ConvDesc& d) {
 }
 
 bool halo_conv_supported(const ConvDesc& d) {
+  static const int off = [] {   // SPK_NO_HALO=1|28|52...: route those convs to the implicit GEMM (experiments)
+    const char* e = std::getenv("SPK_NO_HALO");
+    return e ? std::atoi(e) : 0;
+  }();
   const ConvSrc& s = d.s0;
+  if (off == 1 || (off > 1 && off == s.cin)) return false;
   return s.kh == 3 && s.kw == 3 && s.sh == 1 && s.sw == 1 && s.ph == 1 && s.pw == 1 && s.dh == 1 && s.dw == 1 &&
          !s.reflect && !s.pre_scale && !d.s1.p && d.s1.cin == 0 && d.ksplit == 1 && d.N <= 64 &&
          (s.cin == 28 || s.cin == 32 || s.cin == 52 || s.cin == 64) && d.Ho == s.H && d.Wo == s.W &&
@@ -375,6 +530,9 @@ std::string halo_kernel_name(const ConvDesc& d) {
   int pix = 256, tw = 16;
   pick_tile(d.Ho, d.Wo, np, &pix, &tw);
   const bool add = d.s0.p2 != nullptr || d.s0.ld2 > 0;
+  if (persistent_ok(d) && conv_use_x3() && d.wh && d.wl)
+    return "conv3x3_halo_x3_kernel<" + std::to_string(d.s0.cin) + ", " + std::to_string(tw) + ", " +
+           (add ? "true" : "false") + ">";
   if (persistent_ok(d))
     return "conv3x3_halo_persistent_kernel<" + std::to_string(d.s0.cin) + ", " + std::to_string(tw) + ", " +
            (add ? "true" : "false") + ">";

@@ -434,6 +434,7 @@ hipError_t launch_bk(const ConvDesc& d, const Cfg& c, hipStream_t s) {
 // Name of the kernel instantiation launch_conv() picks (matches rocprofv3 kernel names).
 std::string conv_kernel_name(const ConvDesc& d) {
   if (halo_conv_supported(d)) return halo_kernel_name(d);
+  if (use_x3() && pw_supported(d)) return pw_kernel_name(d);
   const Cfg c = select_cfg(d);
   const bool s1 = d.s1.p != nullptr || d.s1.cin > 0, add = d.s0.p2 != nullptr || d.s0.ld2 > 0;
   const bool pre = d.s0.pre_scale != nullptr;
@@ -451,6 +452,8 @@ int conv_tile_blocks(const ConvDesc& d) {
   return ((M + c.bm - 1) / c.bm) * ((d.N + c.bn - 1) / c.bn);
 }
 
+bool conv_use_x3() { return use_x3(); }
+
 hipError_t launch_conv(const ConvDesc& d, hipStream_t s) {
   // host-side shape checks: every float4 access must stay aligned and in range
   if (d.s0.cin % 4 || d.s0.ld % 4 || (d.s0.p2 && d.s0.ld2 % 4) || d.Kp % KP_ALIGN || d.ldo < d.N ||
@@ -459,6 +462,7 @@ hipError_t launch_conv(const ConvDesc& d, hipStream_t s) {
       d.K > d.Kp || (d.ksplit > 1 && !d.partial))
     return hipErrorInvalidValue;
   if (halo_conv_supported(d)) return launch_conv3x3_halo(d, s);
+  if (use_x3() && pw_supported(d)) return launch_pw(d, s);
   const Cfg c = select_cfg(d);
   return c.bk == 32 ? launch_bk<32>(d, c, s) : launch_bk<16>(d, c, s);
 }
