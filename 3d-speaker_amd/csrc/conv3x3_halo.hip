@@ -286,15 +286,17 @@ conv3x3_halo_persistent_kernel(const ConvDesc d) {
 }
 
 // fp16x3 variant of the persistent kernel (conv_gemm.hip "fp16x3"): the halo and the
-// resident weights are held as fp16 hi / lo planes, channels padded to CINP = 32 (one or two
-// 16-deep k-steps per tap), pixel rows of CINP + 8 halves (conflict-free ds_read_b128).
-// The halo loads are unconditional (clamped address, zero applied from a mask at staging)
-// so they stay in flight across the taps.
-template <int CIN>
+// resident weights are held as fp16 hi / lo planes, channels padded to CINP (a multiple of
+// 16: one 16-deep k-step per 16 channels per tap), pixel rows of CINP + 8 halves
+// (conflict-free ds_read_b128).  A block computes 32 output channels; with N > 32 the
+// channel halves go to the blocks b and b + 8 (same XCD, so the second halo read of a
+// tile is an L2 hit).  The halo loads are unconditional (clamped address, zero applied
+// from a mask at staging) so they stay in flight across the taps.
+template <int CIN, int PIX>
 struct HaloX3Cfg {
-  static constexpr int NP = 32, PIX = 256, NW = 8, NT = 512;
-  static constexpr int CINP = 32, ROW = CINP + 8, QP = CINP / 4, Q = CIN / 4;
-  static constexpr int HALO_PIX = 340;                              // (TH+2)(TW+2), TW in {8, 16, 32}
+  static constexpr int NP = 32, NW = PIX / 32, NT = 64 * NW;
+  static constexpr int CINP = (CIN + 15) / 16 * 16, ROW = CINP + 8, QP = CINP / 4, Q = CIN / 4;
+  static constexpr int HALO_PIX = PIX == 256 ? 340 : 204;          // (TH+2)(TW+2), TW in {8, 16, 32}
   static constexpr int HALO_F = HALO_PIX * ROW;                     // floats = hi + lo halves
   static constexpr int WRES_F = 9 * NP * ROW;                       // floats = hi + lo halves
   static constexpr int EPI = NW * 1024;
@@ -302,10 +304,10 @@ struct HaloX3Cfg {
   static constexpr int PF = (HALO_PIX * QP + NT - 1) / NT;          // staged float4 per thread
 };
 
-template <int CIN, int TW, bool ADD>
-__global__ void __launch_bounds__(512, 1)
-conv3x3_halo_x3_kernel(const ConvDesc d) {
-  using C = HaloX3Cfg<CIN>;
+template <int CIN, int TW, bool ADD, int PIX>
+__global__ void __launch_bounds__(64 * (PIX / 32), 1)
+conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
+  using C = HaloX3Cfg<CIN, PIX>;
   typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
   typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) float lds[C::LDS];
@@ -316,11 +318,17 @@ conv3x3_halo_x3_kernel(const ConvDesc d) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
-  constexpr int TH = C::PIX / TW, HW = TW + 2, HH = TH + 2;
+  constexpr int TH = PIX / TW, HW = TW + 2, HH = TH + 2;
   constexpr int hq = HH * HW * C::QP;
   const int H = d.Ho, W = d.Wo;
   const int ntx = (W + TW - 1) / TW, nty = (H + TH - 1) / TH;
   const int ntiles = d.nimg * ntx * nty;
+  // channel slice: blocks b and b+8 (one XCD) share tiles, one per 32-channel slice
+  const int b = blockIdx.x;
+  const int slice = nsplit > 1 ? (b >> 3) % nsplit : 0;
+  const int tbase = nsplit > 1 ? (b & 7) + 8 * (b / (8 * nsplit)) : b;
+  const int tstride = gridDim.x / nsplit;
+  const int n0 = slice * C::NP;
 
   f32x4 pa[C::PF], pb[ADD ? C::PF : 1];
   unsigned pok = 0;
@@ -363,15 +371,15 @@ conv3x3_halo_x3_kernel(const ConvDesc d) {
     }
   };
 
-  int t = blockIdx.x;
+  int t = tbase;
   if (t < ntiles) pf_load(t);
-  // all nine taps of the split weights -> LDS ([tap][n][ROW] hi / lo); channels >= CIN zero
+  // all nine taps of this slice's split weights -> LDS ([tap][n][ROW] hi / lo); zero padded
   for (int idx = tid; idx < 9 * C::NP * C::QP; idx += C::NT) {
     const int q = idx % C::QP, n = (idx / C::QP) % C::NP, tap = idx / (C::QP * C::NP);
     typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
     u16x4 h = {0, 0, 0, 0}, l = {0, 0, 0, 0};
-    if (n < d.N && q < C::Q) {
-      const size_t o = (size_t)n * d.Kp + tap * CIN + 4 * q;
+    if (n0 + n < d.N && q < C::Q) {
+      const size_t o = (size_t)(n0 + n) * d.Kp + tap * CIN + 4 * q;
       h = *reinterpret_cast<const u16x4*>(d.wh + o);
       l = *reinterpret_cast<const u16x4*>(d.wl + o);
     }
@@ -384,8 +392,8 @@ conv3x3_halo_x3_kernel(const ConvDesc d) {
   const int p_own = wave * 32 + li;
   const int abase = ((p_own / TW) * HW + (p_own % TW)) * C::ROW + 8 * lh;
   const int bbase = li * C::ROW + 8 * lh;
-  for (; t < ntiles; t += gridDim.x) {
-    const int tn = t + gridDim.x;
+  for (; t < ntiles; t += tstride) {
+    const int tn = t + tstride;
     if (tn < ntiles) pf_load(tn);                   // in flight during the taps and epilogue
     f32x16 acc[1][1], accx;
 #pragma unroll
@@ -410,7 +418,7 @@ conv3x3_halo_x3_kernel(const ConvDesc d) {
     {
       const int img = t / (ntx * nty), ty = (t / ntx) % nty, tx = t % ntx;
       const int y0 = ty * TH, x0 = tx * TW;
-      epilogue_tiles<1, 1, true>(d, lds, acc, wave, lane, 0, d.nimg * H * W, [&](int r) {
+      epilogue_tiles<1, 1, true>(d, lds, acc, wave, lane, n0, d.nimg * H * W, [&](int r) {
         const int p = wave * 32 + r;
         const int gy = y0 + p / TW, gx = x0 + p % TW;
         return (gy < H && gx < W) ? (img * H + gy) * W + gx : -1;
@@ -442,22 +450,40 @@ int resident_blocks(K kernel, int threads) {
   return n;
 }
 
+template <int CIN, int TW, int PIX>
+hipError_t launch_halo_x3_tw(const ConvDesc& d, hipStream_t s) {
+  constexpr int TH = PIX / TW, NT = 64 * (PIX / 32);
+  const int tiles = d.nimg * ((d.Ho + TH - 1) / TH) * ((d.Wo + TW - 1) / TW);
+  const int nsplit = (d.N + 31) / 32;
+  auto grid_for = [&](int per_cu) {
+    // nsplit blocks per tile group of 8; a multiple of 8 * nsplit (or everything when small)
+    const int slots = per_cu * device_cus();
+    const int g = std::min((tiles + 7) / 8 * 8, std::max(8, slots / nsplit / 8 * 8));
+    return g * nsplit;
+  };
+  if (d.s0.p2) {
+    auto k = conv3x3_halo_x3_kernel<CIN, TW, true, PIX>;
+    static const int per_cu = resident_blocks(k, NT);
+    hipLaunchKernelGGL(k, dim3(grid_for(per_cu)), dim3(NT), 0, s, d, nsplit);
+  } else {
+    auto k = conv3x3_halo_x3_kernel<CIN, TW, false, PIX>;
+    static const int per_cu = resident_blocks(k, NT);
+    hipLaunchKernelGGL(k, dim3(grid_for(per_cu)), dim3(NT), 0, s, d, nsplit);
+  }
+  return hipGetLastError();
+}
+
+template <int CIN, int PIX>
+hipError_t launch_halo_x3(const ConvDesc& d, int TW, hipStream_t s) {
+  if (TW == 8) return launch_halo_x3_tw<CIN, 8, PIX>(d, s);
+  if (TW == 16) return launch_halo_x3_tw<CIN, 16, PIX>(d, s);
+  return launch_halo_x3_tw<CIN, 32, PIX>(d, s);
+}
+
 template <int CIN, int TW>
 hipError_t launch_halo_persistent_tw(const ConvDesc& d, hipStream_t s) {
   constexpr int TH = 256 / TW;
   const int tiles = d.nimg * ((d.Ho + TH - 1) / TH) * ((d.Wo + TW - 1) / TW);
-  if (conv_use_x3() && d.wh && d.wl) {
-    if (d.s0.p2) {
-      auto k = conv3x3_halo_x3_kernel<CIN, TW, true>;
-      static const int per_cu = resident_blocks(k, 512);
-      hipLaunchKernelGGL(k, dim3(std::min(tiles, per_cu * device_cus())), dim3(512), 0, s, d);
-    } else {
-      auto k = conv3x3_halo_x3_kernel<CIN, TW, false>;
-      static const int per_cu = resident_blocks(k, 512);
-      hipLaunchKernelGGL(k, dim3(std::min(tiles, per_cu * device_cus())), dim3(512), 0, s, d);
-    }
-    return hipGetLastError();
-  }
   if (d.s0.p2) {
     auto k = conv3x3_halo_persistent_kernel<CIN, TW, true>;
     static const int per_cu = resident_blocks(k, 512);
@@ -506,6 +532,24 @@ void pick_tile(int H, int W, int np, int* pix, int* tw) {
 
 }  // namespace
 
+// the x3 kernel: lean epilogue (conv_epilogue.h), <= 64 output channels as 32-channel slices
+bool x3_halo_ok(const ConvDesc& d) {
+  return conv_use_x3() && d.wh && d.wl && d.N <= 64 && d.N % 4 == 0 && d.ldo % 4 == 0 &&
+         (!d.res || d.ldr % 4 == 0) && !d.affx && !d.gate && !d.rowbias && d.ksplit == 1;
+}
+
+// tile width for a fixed pixel count: least edge waste
+int pick_tw(int H, int W, int P) {
+  double best = 1e30;
+  int tw = 16;
+  for (int t : {8, 16, 32}) {
+    const int th = P / t;
+    const double cover = (double)((H + th - 1) / th) * th * ((W + t - 1) / t) * t;
+    if (cover < best - 1e-9) { best = cover; tw = t; }
+  }
+  return tw;
+}
+
 // the persistent kernel: <= 32 output channels and the lean epilogue (conv_epilogue.h)
 bool persistent_ok(const ConvDesc& d) {
   return d.N <= 32 && (d.s0.cin == 28 || d.s0.cin == 32) && d.N % 4 == 0 && d.ldo % 4 == 0 &&
@@ -530,9 +574,11 @@ std::string halo_kernel_name(const ConvDesc& d) {
   int pix = 256, tw = 16;
   pick_tile(d.Ho, d.Wo, np, &pix, &tw);
   const bool add = d.s0.p2 != nullptr || d.s0.ld2 > 0;
-  if (persistent_ok(d) && conv_use_x3() && d.wh && d.wl)
-    return "conv3x3_halo_x3_kernel<" + std::to_string(d.s0.cin) + ", " + std::to_string(tw) + ", " +
-           (add ? "true" : "false") + ">";
+  if (x3_halo_ok(d)) {
+    const int px = d.s0.cin <= 32 ? 256 : 128;
+    return "conv3x3_halo_x3_kernel<" + std::to_string(d.s0.cin) + ", " + std::to_string(pick_tw(d.Ho, d.Wo, px)) +
+           ", " + (add ? "true" : "false") + ", " + std::to_string(px) + ">";
+  }
   if (persistent_ok(d))
     return "conv3x3_halo_persistent_kernel<" + std::to_string(d.s0.cin) + ", " + std::to_string(tw) + ", " +
            (add ? "true" : "false") + ">";
@@ -549,6 +595,12 @@ hipError_t launch_conv3x3_halo(const ConvDesc& d, hipStream_t s) {
   if (d.s0.cin == CI) {                                                                 \
     if (np == 32) return launch_halo_t<CI, 32, 256>(d, tw, s);                          \
     return pix == 256 ? launch_halo_t<CI, 64, 256>(d, tw, s) : launch_halo_t<CI, 64, 128>(d, tw, s); \
+  }
+  if (x3_halo_ok(d)) {
+    if (d.s0.cin == 28) return launch_halo_x3<28, 256>(d, pick_tw(d.Ho, d.Wo, 256), s);
+    if (d.s0.cin == 32) return launch_halo_x3<32, 256>(d, pick_tw(d.Ho, d.Wo, 256), s);
+    if (d.s0.cin == 52) return launch_halo_x3<52, 128>(d, pick_tw(d.Ho, d.Wo, 128), s);
+    if (d.s0.cin == 64) return launch_halo_x3<64, 128>(d, pick_tw(d.Ho, d.Wo, 128), s);
   }
   if (persistent_ok(d) && d.s0.cin == 28) return launch_halo_persistent<28>(d, tw, s);
   if (persistent_ok(d) && d.s0.cin == 32) return launch_halo_persistent<32>(d, tw, s);
