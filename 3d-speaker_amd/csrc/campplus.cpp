@@ -58,11 +58,16 @@ void build_campplus(Builder& b, int T) {
     const float* bias = m.dptr(stem.b_off);
     const int kp = stem.Kp;
     const Buf xo = x.buf;
+    const bool rg = b.ragged;
     b.step("head.stem", [=](const Ctx& c) {
-      return launch_stem_conv3x3(c.in, B, T, F, w, bias, mc, ACT_RELU, kp, c.resolve(xo), mc, c.stream);
+      return launch_stem_conv3x3(c.in, B, T, F, w, bias, mc, ACT_RELU, kp, c.resolve(xo), mc, c.stream,
+                                 rg ? c.lens : nullptr);
     });
   }
   const ChanMap cm = ChanMap::dense(mc);
+  // ragged batches: outputs past an utterance's valid frames are written as zero, so every
+  // conv sees the zero padding of that utterance alone; BN-ReLU'd inputs are masked on load
+  const Buf LENS = b.ragged ? Buf{Buf::LEN, 0, nullptr} : Buf{};
   // FCM BasicResBlocks
   for (int li = 1; li <= 2; ++li) {
     for (int bi = 0; bi < 2; ++bi) {
@@ -86,13 +91,13 @@ void build_campplus(Builder& b, int T) {
         d.nimg = B; d.Ho = Ho; d.Wo = T;
         d.s0 = src2d(x, mc, 3, 3, stride, 1, 1, 1);
         d.ldo = mc; d.act = ACT_RELU;
-        Builder::ConvIO io; io.s0 = x.buf; io.out = y1.buf;
+        Builder::ConvIO io; io.s0 = x.buf; io.out = y1.buf; io.rowlen = LENS;
         b.conv(p + ".conv1", d, c1, io);
         b.macs_per_utt += macs2;
         ConvDesc e;
         e.nimg = B; e.Ho = Ho; e.Wo = T;
         e.s0 = src2d(y1, mc, 3, 3, 1, 1, 1, 1);
-        Builder::ConvIO io2; io2.s0 = y1.buf; io2.out = out.buf;
+        Builder::ConvIO io2; io2.s0 = y1.buf; io2.out = out.buf; io2.rowlen = LENS;
         if (sc) {
           e.s1 = src2d(x, mc, 1, 1, stride, 1, 0, 0);
           io2.s1 = x.buf;
@@ -117,7 +122,7 @@ void build_campplus(Builder& b, int T) {
       d.nimg = B; d.Ho = Ho; d.Wo = T;
       d.s0 = src2d(x, mc, 3, 3, 2, 1, 1, 1);
       d.ldo = mc; d.act = ACT_RELU;
-      Builder::ConvIO io; io.s0 = x.buf; io.out = z.buf;
+      Builder::ConvIO io; io.s0 = x.buf; io.out = z.buf; io.rowlen = LENS;
       b.conv("head.conv2", d, c, io);
     }
     x = z;
@@ -143,6 +148,17 @@ void build_campplus(Builder& b, int T) {
     m.shapes[tk2] = t.shape;
   }
   const int T2 = (T + 2 * (K5 / 2) - K5) / 2 + 1;
+  // valid frames after the stride-2 TDNN, per utterance (ragged batches)
+  Buf LEN2;
+  if (b.ragged) {
+    LEN2 = b.alloc((size_t)B);
+    if (b.plan) {
+      const int pad = K5 / 2, k5 = K5;
+      b.step("xvector.tdnn.lengths", [=](const Ctx& c) {
+        return launch_derive_len(c.lens, c.resolve_i(LEN2), B, pad, k5, 2, c.stream);
+      });
+    }
+  }
   const double T2d = T2;
   const int nseg = (T2 + 99) / 100;
   // dense blocks: sizes
@@ -175,7 +191,7 @@ void build_campplus(Builder& b, int T) {
       d.nimg = B; d.Ho = 1; d.Wo = T2;
       d.s0 = src2d(x, mc, Fh, K5, 1, 2, 0, K5 / 2);
       d.ldo = blks[0].c_fin; d.act = ACT_RELU;
-      Builder::ConvIO io; io.s0 = x.buf; io.out = blks[0].buf;
+      Builder::ConvIO io; io.s0 = x.buf; io.out = blks[0].buf; io.rowlen = LEN2;
       b.conv("xvector.tdnn", d, p, io);
     }
   }
@@ -222,12 +238,13 @@ void build_campplus(Builder& b, int T) {
         d.s0.pre_scale = m.dptr(pre->ps_off);
         d.s0.pre_shift = m.dptr(pre->pt_off);
         d.ldo = bnc; d.act = ACT_RELU;
-        Builder::ConvIO io; io.s0 = bk.buf; io.out = Hh;
+        Builder::ConvIO io; io.s0 = bk.buf; io.out = Hh; io.vlen = LEN2; io.rowlen = LEN2;
         b.macs_per_utt += m_l1;
         b.conv(q + ".linear1", d, l1, io);
       }
       b.step(c + ".context", [=](const Ctx& cx) {
-        return launch_cam_context(cx.resolve(Hh), B, T2, bnc, bnc, 100, nseg, cx.resolve(CTX), bnc, cx.stream);
+        return launch_cam_context(cx.resolve(Hh), B, T2, bnc, bnc, 100, nseg, cx.resolve(CTX), bnc, cx.stream,
+                                  cx.resolve_i(LEN2));
       });
       {
         ConvDesc d;
@@ -254,7 +271,7 @@ void build_campplus(Builder& b, int T) {
         d.s0 = src2d(hh, bnc, 1, ks, 1, 1, 0, (ks - 1) / 2 * bk.d, bk.d);
         d.ldo = bk.c_fin;
         d.gate_ld = growth; d.gate_seg = 100; d.gate_nseg = nseg;
-        Builder::ConvIO io; io.s0 = Hh; io.out = bk.buf.at((size_t)cin); io.gate = GATE;
+        Builder::ConvIO io; io.s0 = Hh; io.out = bk.buf.at((size_t)cin); io.gate = GATE; io.rowlen = LEN2;
         b.macs_per_utt += m_loc;
         b.conv(c + ".linear_local", d, loc, io);
       }
@@ -290,7 +307,7 @@ void build_campplus(Builder& b, int T) {
       d.s0.pre_shift = m.dptr(pre->pt_off);
       d.ldo = ldd;
       if (last) d.act = ACT_RELU;
-      Builder::ConvIO io; io.s0 = bk.buf; io.out = dst;
+      Builder::ConvIO io; io.s0 = bk.buf; io.out = dst; io.vlen = LEN2; io.rowlen = LEN2;
       b.conv(t, d, tp, io, /*use_bias=*/last);
     }
   }
@@ -305,7 +322,8 @@ void build_campplus(Builder& b, int T) {
   b.macs_per_utt += (double)E * 2 * c_final;
   if (!b.plan) return;
   b.step("xvector.stats", [=](const Ctx& c) {
-    return launch_stats_pool(c.resolve(xo_final), B, T2, c_final, c_final, c.resolve(ST), c.stream);
+    return launch_stats_pool(c.resolve(xo_final), B, T2, c_final, c_final, c.resolve(ST), c.stream,
+                             c.resolve_i(LEN2));
   });
   ConvDesc d;
   d.nimg = B; d.Ho = 1; d.Wo = 1;

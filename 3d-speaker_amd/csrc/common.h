@@ -34,6 +34,9 @@ struct ConvSrc {
   // activated tensor)
   const float* pre_scale = nullptr;
   const float* pre_shift = nullptr;
+  // optional per-image valid width (ragged batches: time axis = W): positions w >= vlen[img]
+  // read as padding (zero), exactly like the end of an utterance of that length
+  const int* vlen = nullptr;
 };
 
 // out[m, n] = epi( sum_k A[m, k] * Wt[n, k] ), m = (img, ho, wo), k = (tap, c) of s0 then c of s1.
@@ -58,7 +61,15 @@ struct ConvDesc {
   const float* gate = nullptr; int gate_ld = 0; int gate_seg = 0;  // out *= gate[img][t/seg][n] (CAM)
   int gate_nseg = 0;
   int ksplit = 1; float* partial = nullptr;            // split-K partial slabs [ksplit][M][N]
+  const int* rowlen = nullptr;  // ragged batches: outputs with wo >= rowlen[img] are written as 0
 };
+
+// true when output row m is past its image's valid length (ragged batches)
+__host__ __device__ inline bool row_masked(const ConvDesc& d, int m) {
+  if (!d.rowlen) return false;
+  const int wo = m % d.Wo, img = m / (d.Wo * d.Ho);
+  return wo >= d.rowlen[img];
+}
 
 hipError_t launch_conv(const ConvDesc& d, hipStream_t s);
 bool conv_use_x3();   // fp16x3 split-precision MFMA path (default; SPK_CONV_MFMA=f32 selects exact fp32 MFMA)

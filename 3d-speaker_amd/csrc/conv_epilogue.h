@@ -41,7 +41,7 @@ __device__ __forceinline__ float epilogue_elem(const ConvDesc& d, int m, int n, 
     const int img = m / (d.Wo * d.Ho);
     v *= d.gate[((size_t)img * d.gate_nseg + wo / d.gate_seg) * d.gate_ld + n];
   }
-  return v;
+  return row_masked(d, m) ? 0.f : v;
 }
 
 
@@ -118,6 +118,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
             if (d.post_scale) x = x * ps[e] + pt[e];
             o[e] = apply_act(x, d.act2);
           }
+          if (row_masked(d, m)) o = f32x4{0.f, 0.f, 0.f, 0.f};
           *reinterpret_cast<f32x4*>(d.out + (size_t)m * d.ldo + n) = o;
         }
       }
@@ -189,6 +190,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
                 o *= *reinterpret_cast<const f32x4*>(d.gate + ((size_t)img * d.gate_nseg + wo / d.gate_seg) * d.gate_ld + n);
               }
             }
+            if (row_masked(d, m)) o = f32x4{0.f, 0.f, 0.f, 0.f};
             *reinterpret_cast<f32x4*>(d.out + (size_t)m * d.ldo + n) = o;
           }
         }

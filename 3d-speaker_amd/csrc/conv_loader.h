@@ -74,7 +74,8 @@ struct ALoader {
         hi = hi < 0 ? -hi : (hi >= d.s0.H ? 2 * d.s0.H - 2 - hi : hi);
         wi = wi < 0 ? -wi : (wi >= d.s0.W ? 2 * d.s0.W - 2 - wi : wi);
       }
-      const bool ok0 = in0 && ((rok >> r) & 1) && hi >= 0 && hi < d.s0.H && wi >= 0 && wi < d.s0.W;
+      const bool ok0 = in0 && ((rok >> r) & 1) && hi >= 0 && hi < d.s0.H && wi >= 0 && wi < d.s0.W &&
+                       (!d.s0.vlen || wi < d.s0.vlen[img[r]]);
       const bool ok1 = in1 && ((rok >> r) & 1);
       // offsets computed unconditionally and selected (branch-free)
       const long long pix0 = (long long)(img[r] * d.s0.H + hi) * d.s0.W + wi;

@@ -17,8 +17,10 @@ struct FbankTables {
 // of mel weights used; -1 if n_mels is unsupported.
 int build_fbank_tables(FbankTables* t, int n_mels, double sample_rate);
 
+// t_max > 0: utterance u is written at rows [u * t_max, u * t_max + frames_u), the rest of
+// its t_max rows zeroed (a padded [n_utt, t_max, n_mels] batch); frame_off still gives frames_u
 hipError_t launch_fbank(const float* wav, const int64_t* wav_off, int n_utt, float* feats,
                         const int64_t* frame_off, int n_mels, int mean_nor, const FbankTables* tab,
-                        hipStream_t s);
+                        hipStream_t s, int t_max = 0);
 
 }  // namespace spk

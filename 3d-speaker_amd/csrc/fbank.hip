@@ -38,7 +38,7 @@ __device__ __forceinline__ int bitrev9(int x) { return __builtin_bitreverse32((u
 __global__ void __launch_bounds__(256)
 fbank_kernel(const float* __restrict__ wav, const int64_t* __restrict__ wav_off,
              float* __restrict__ feats, const int64_t* __restrict__ frame_off,
-             const FbankTables* __restrict__ tab, int n_mels, int mean_nor) {
+             const FbankTables* __restrict__ tab, int n_mels, int mean_nor, int t_max) {
   __shared__ float2 buf[WAVES][NFFT];
   __shared__ float pw[WAVES][HALF + 1];
   __shared__ float colsum[WAVES][128];
@@ -46,9 +46,13 @@ fbank_kernel(const float* __restrict__ wav, const int64_t* __restrict__ wav_off,
   const int utt = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float* x = wav + wav_off[utt];
-  const int64_t f0 = frame_off[utt];
-  const int nfr = (int)(frame_off[utt + 1] - f0);
+  const int nfr = (int)(frame_off[utt + 1] - frame_off[utt]);
+  // packed (t_max == 0): rows at frame_off[utt]; padded: rows at utt * t_max, rows
+  // [nfr, t_max) of the utterance zeroed
+  const int64_t f0 = t_max > 0 ? (int64_t)utt * t_max : frame_off[utt];
   float* out = feats + f0 * n_mels;
+  if (t_max > 0)
+    for (int e = nfr * n_mels + threadIdx.x; e < t_max * n_mels; e += blockDim.x) out[e] = 0.f;
 
   float cs0 = 0.f, cs1 = 0.f;   // column sums for mel bins lane, lane+64
   for (int fr = wave; fr < nfr; fr += WAVES) {
@@ -141,11 +145,11 @@ fbank_kernel(const float* __restrict__ wav, const int64_t* __restrict__ wav_off,
 
 hipError_t launch_fbank(const float* wav, const int64_t* wav_off, int n_utt, float* feats,
                         const int64_t* frame_off, int n_mels, int mean_nor, const FbankTables* tab,
-                        hipStream_t s) {
-  if (n_mels <= 0 || n_mels > 128 || n_utt < 0) return hipErrorInvalidValue;
+                        hipStream_t s, int t_max) {
+  if (n_mels <= 0 || n_mels > 128 || n_utt < 0 || t_max < 0) return hipErrorInvalidValue;
   if (n_utt == 0) return hipSuccess;
   hipLaunchKernelGGL(fbank_kernel, dim3(n_utt), dim3(256), 0, s, wav, wav_off, feats, frame_off, tab, n_mels,
-                     mean_nor);
+                     mean_nor, t_max);
   return hipGetLastError();
 }
 

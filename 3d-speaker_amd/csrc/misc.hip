@@ -15,7 +15,7 @@ namespace {
 __global__ void __launch_bounds__(256)
 stem_conv3x3_kernel(const float* __restrict__ feats, int B, int T, int F, const float* __restrict__ w,
                     const float* __restrict__ bias, int cout, int act, int wstride, float* __restrict__ out,
-                    int ldo) {
+                    int ldo, const int* __restrict__ vlen) {
   // thread -> (pixel, 16 output channels); pixel = (b, f, t) of the (F, T) image.  Weights and
   // bias are staged in LDS once per block; 32-bit index math only.
   __shared__ float ws[128 * 9];
@@ -32,14 +32,16 @@ stem_conv3x3_kernel(const float* __restrict__ feats, int B, int T, int F, const 
     const int bf = pix / T;
     const int f = bf % F;
     const int b = bf / F;
+    const int Tb = vlen ? vlen[b] : T;               // ragged batches: frames past Tb are padding
     float in[9];
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
       for (int dx = 0; dx < 3; ++dx) {
         const int ff = f + dy - 1, tt = t + dx - 1;
-        in[dy * 3 + dx] = (ff >= 0 && ff < F && tt >= 0 && tt < T) ? feats[(b * T + tt) * F + ff] : 0.f;
+        in[dy * 3 + dx] = (ff >= 0 && ff < F && tt >= 0 && tt < Tb) ? feats[(b * T + tt) * F + ff] : 0.f;
       }
+    const bool dead = t >= Tb;
     float* op = out + (size_t)pix * ldo + g * 16;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -52,7 +54,7 @@ stem_conv3x3_kernel(const float* __restrict__ feats, int B, int T, int F, const 
 #pragma unroll
         for (int k = 0; k < 9; ++k) acc = fmaf(in[k], ws[c * 9 + k], acc);
         acc += bs[c];
-        ov[j] = act == ACT_RELU ? fmaxf(acc, 0.f) : acc;
+        ov[j] = dead ? 0.f : (act == ACT_RELU ? fmaxf(acc, 0.f) : acc);
       }
       *reinterpret_cast<float4*>(op + q * 4) = o;
     }
@@ -88,13 +90,13 @@ tstp_kernel(const float* __restrict__ x, int B, int H, int W, int C, int ld, flo
 }  // namespace
 
 hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const float* w, const float* bias, int cout,
-                               int act, int wstride, float* out, int ldo, hipStream_t s) {
+                               int act, int wstride, float* out, int ldo, hipStream_t s, const int* vlen) {
   if (cout % 16 || cout > 128 || ldo % 4 || (long long)B * F * T * (cout / 16) >= (1LL << 31))
     return hipErrorInvalidValue;
   const long long total = (long long)B * F * T * (cout / 16);
   const int blocks = (int)std::min<long long>((total + 255) / 256, 65536);
   hipLaunchKernelGGL(stem_conv3x3_kernel, dim3(blocks), dim3(256), 0, s, feats, B, T, F, w, bias, cout, act, wstride, out,
-                     ldo);
+                     ldo, vlen);
   return hipGetLastError();
 }
 

@@ -176,6 +176,9 @@ void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const C
   ConvDesc probe = d;   // kernel label: same tile choice as launch_conv
   probe.s1.cin = io.s1 ? d.s1.cin : 0;
   probe.s0.ld2 = io.s0b ? std::max(d.s0.ld2, 1) : 0;
+  static const int kDummyLen = 0;   // naming probe only: marks the ragged masks as present
+  probe.rowlen = io.rowlen ? &kDummyLen : nullptr;
+  probe.s0.vlen = io.vlen ? &kDummyLen : nullptr;
   step(name, [d, cio](const Ctx& c) mutable {
     d.s0.p = c.resolve(cio.s0);
     d.s0.p2 = c.resolve(cio.s0b);
@@ -187,6 +190,8 @@ void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const C
     d.gate = c.resolve(cio.gate);
     d.partial = c.resolve(cio.partial);
     d.rowbias = c.resolve(cio.rowbias);
+    d.rowlen = c.resolve_i(cio.rowlen);
+    d.s0.vlen = c.resolve_i(cio.vlen);
     return launch_conv(d, c.stream);
   }, conv_kernel_name(probe));
 }
@@ -225,13 +230,15 @@ int hip_check(hipError_t e, const char* what) {
   return SPK_E_HIP;
 }
 
-Plan* get_plan(spk_model_t* h, int B, int T, double* macs = nullptr) {
+Plan* get_plan(spk_model_t* h, int B, int T, bool ragged = false) {
   std::lock_guard<std::mutex> lk(h->m.mu);
-  auto key = std::make_pair(B, T);
+  auto key = std::make_pair(B, ragged ? -T : T);
   auto it = h->m.plans.find(key);
   if (it != h->m.plans.end()) return it->second.get();
+  if (ragged && h->m.cfg.arch != SPK_ARCH_CAMPPLUS)
+    throw SpkError(SPK_E_UNSUPPORTED, "per-utterance lengths are implemented for CAM++ only");
   auto plan = std::make_unique<Plan>();
-  Builder b(h->m, plan.get(), B);
+  Builder b(h->m, plan.get(), B, ragged);
   switch (h->m.cfg.arch) {
     case SPK_ARCH_ERES2NETV2: build_eres2net(b, T, true); break;
     case SPK_ARCH_ERES2NET: build_eres2net(b, T, false); break;
@@ -240,7 +247,6 @@ Plan* get_plan(spk_model_t* h, int B, int T, double* macs = nullptr) {
     default: throw SpkError(SPK_E_UNSUPPORTED, "unknown arch");
   }
   plan->ws_bytes = b.ws;
-  (void)macs;
   Plan* p = plan.get();
   h->m.plans.emplace(key, std::move(plan));
   return p;
@@ -254,8 +260,8 @@ int spk_version(void) { return 1; }
 
 const char* spk_last_error(void) { return g_last_error.c_str(); }
 
-int spk_fbank_f32(const float* wav, const int64_t* wav_offsets, int32_t n_utt, float* feats,
-                  const int64_t* frame_offsets, int32_t n_mels, int32_t mean_nor, void* stream) {
+static int fbank_impl(const float* wav, const int64_t* wav_offsets, int32_t n_utt, float* feats,
+                      const int64_t* frame_offsets, int32_t n_mels, int32_t mean_nor, void* stream, int32_t t_max) {
   return guarded([&]() -> int {
     if (n_utt < 0 || n_mels <= 3 || n_mels > 128 || (n_utt > 0 && (!wav || !wav_offsets || !feats || !frame_offsets))) {
       set_error("spk_fbank_f32: invalid argument");
@@ -284,9 +290,23 @@ int spk_fbank_f32(const float* wav, const int64_t* wav_offsets, int32_t n_utt, f
       tab = g_tables[dev];
     }
     return hip_check(launch_fbank(wav, wav_offsets, n_utt, feats, frame_offsets, n_mels, mean_nor, tab,
-                                  reinterpret_cast<hipStream_t>(stream)),
+                                  reinterpret_cast<hipStream_t>(stream), t_max),
                      "fbank launch");
   });
+}
+
+int spk_fbank_f32(const float* wav, const int64_t* wav_offsets, int32_t n_utt, float* feats,
+                  const int64_t* frame_offsets, int32_t n_mels, int32_t mean_nor, void* stream) {
+  return fbank_impl(wav, wav_offsets, n_utt, feats, frame_offsets, n_mels, mean_nor, stream, 0);
+}
+
+int spk_fbank_f32_padded(const float* wav, const int64_t* wav_offsets, int32_t n_utt, float* feats,
+                         const int64_t* frame_offsets, int32_t t_max, int32_t n_mels, int32_t mean_nor, void* stream) {
+  if (t_max <= 0) {
+    set_error("spk_fbank_f32_padded: t_max must be > 0");
+    return SPK_E_INVALID;
+  }
+  return fbank_impl(wav, wav_offsets, n_utt, feats, frame_offsets, n_mels, mean_nor, stream, t_max);
 }
 
 int spk_model_create(const spk_model_config_t* cfg, const spk_weight_t* weights, int32_t n_weights, spk_model_t** out) {
@@ -392,33 +412,57 @@ int spk_model_flops(spk_model_t* model, int32_t T, double* flops) {
   });
 }
 
+static int run_forward(const char* fn, spk_model_t* model, const float* feats, int32_t B, int32_t T,
+                       const int32_t* lengths, void* workspace, size_t workspace_bytes, float* emb_out, void* stream) {
+  if (!model || !feats || !emb_out || B <= 0 || T <= 0) {
+    set_error(std::string(fn) + ": invalid argument");
+    return SPK_E_INVALID;
+  }
+  int dev = 0;
+  if (int rc = hip_check(hipGetDevice(&dev), "hipGetDevice")) return rc;
+  if (dev != model->m.device) {
+    set_error(std::string(fn) + ": handle belongs to another device");
+    return SPK_E_DEVICE;
+  }
+  Plan* plan = get_plan(model, B, T, lengths != nullptr);
+  if (workspace_bytes < plan->ws_bytes || (plan->ws_bytes && !workspace)) {
+    set_error(std::string(fn) + ": workspace too small (need " + std::to_string(plan->ws_bytes) + " bytes)");
+    return SPK_E_WORKSPACE;
+  }
+  Ctx c{reinterpret_cast<char*>(workspace), feats, emb_out, reinterpret_cast<hipStream_t>(stream), lengths};
+  for (size_t i = 0; i < plan->steps.size(); ++i) {
+    hipError_t e = plan->steps[i](c);
+    if (e != hipSuccess) {
+      set_error(std::string(fn) + ": step '" + plan->names[i] + "': " + hipGetErrorString(e));
+      return SPK_E_HIP;
+    }
+  }
+  return SPK_OK;
+}
+
 int spk_model_forward(spk_model_t* model, const float* feats, int32_t B, int32_t T, void* workspace,
                       size_t workspace_bytes, float* emb_out, void* stream) {
   return guarded([&]() -> int {
-    if (!model || !feats || !emb_out || B <= 0 || T <= 0) {
-      set_error("spk_model_forward: invalid argument");
+    return run_forward("spk_model_forward", model, feats, B, T, nullptr, workspace, workspace_bytes, emb_out, stream);
+  });
+}
+
+int spk_model_workspace_bytes_lengths(spk_model_t* model, int32_t B, int32_t T, int32_t ragged, size_t* bytes) {
+  return guarded([&]() -> int {
+    if (!model || !bytes || B <= 0 || T <= 0) {
+      set_error("spk_model_workspace_bytes_lengths: invalid argument");
       return SPK_E_INVALID;
     }
-    int dev = 0;
-    if (int rc = hip_check(hipGetDevice(&dev), "hipGetDevice")) return rc;
-    if (dev != model->m.device) {
-      set_error("spk_model_forward: handle belongs to another device");
-      return SPK_E_DEVICE;
-    }
-    Plan* plan = get_plan(model, B, T);
-    if (workspace_bytes < plan->ws_bytes || (plan->ws_bytes && !workspace)) {
-      set_error("spk_model_forward: workspace too small (need " + std::to_string(plan->ws_bytes) + " bytes)");
-      return SPK_E_WORKSPACE;
-    }
-    Ctx c{reinterpret_cast<char*>(workspace), feats, emb_out, reinterpret_cast<hipStream_t>(stream)};
-    for (size_t i = 0; i < plan->steps.size(); ++i) {
-      hipError_t e = plan->steps[i](c);
-      if (e != hipSuccess) {
-        set_error("spk_model_forward: step '" + plan->names[i] + "': " + hipGetErrorString(e));
-        return SPK_E_HIP;
-      }
-    }
+    *bytes = get_plan(model, B, T, ragged != 0)->ws_bytes;
     return SPK_OK;
+  });
+}
+
+int spk_model_forward_lengths(spk_model_t* model, const float* feats, int32_t B, int32_t T, const int32_t* lengths,
+                              void* workspace, size_t workspace_bytes, float* emb_out, void* stream) {
+  return guarded([&]() -> int {
+    return run_forward("spk_model_forward_lengths", model, feats, B, T, lengths, workspace, workspace_bytes, emb_out,
+                       stream);
   });
 }
 

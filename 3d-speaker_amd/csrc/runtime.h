@@ -21,7 +21,7 @@ struct SpkError : std::runtime_error {
 // A pointer resolved at launch time: into the caller's workspace, the input features, the
 // output embeddings, or the model's packed weights (absolute).
 struct Buf {
-  enum Kind { NONE = 0, WS = 1, IN = 2, OUT = 3, ABS = 4 };
+  enum Kind { NONE = 0, WS = 1, IN = 2, OUT = 3, ABS = 4, LEN = 5 };   // LEN: caller's per-utterance frames
   int kind = NONE;
   size_t off = 0;           // bytes (WS/IN/OUT) ; ABS uses ptr
   const float* ptr = nullptr;
@@ -34,15 +34,18 @@ struct Ctx {
   const float* in;
   float* out;
   hipStream_t stream;
+  const int* lens = nullptr;   // ragged batches: valid frames per utterance (device int32 [B])
   float* resolve(const Buf& b) const {
     switch (b.kind) {
       case Buf::WS: return reinterpret_cast<float*>(ws + b.off);
       case Buf::IN: return const_cast<float*>(reinterpret_cast<const float*>(reinterpret_cast<const char*>(in) + b.off));
       case Buf::OUT: return reinterpret_cast<float*>(reinterpret_cast<char*>(out) + b.off);
       case Buf::ABS: return const_cast<float*>(b.ptr);
+      case Buf::LEN: return lens ? reinterpret_cast<float*>(const_cast<int*>(lens)) : nullptr;
       default: return nullptr;
     }
   }
+  int* resolve_i(const Buf& b) const { return reinterpret_cast<int*>(resolve(b)); }
 };
 
 using Step = std::function<hipError_t(const Ctx&)>;
@@ -94,7 +97,7 @@ struct Model {
   size_t dweights_bytes = 0;
   uint16_t* dsplit = nullptr;                     // fp16 hi plane then lo plane of the whole arena
   std::map<std::string, Packed> packed;
-  std::map<std::pair<int, int>, std::unique_ptr<Plan>> plans;
+  std::map<std::pair<int, int>, std::unique_ptr<Plan>> plans;   // key (B, T) ; ragged plans use -T
   std::mutex mu;
   bool uploaded = false;
 
@@ -122,12 +125,14 @@ struct Builder {
   size_t ws = 0;
   double macs_per_utt = 0;   // algorithmic conv/linear MACs for this (T)
   double macs_at_last_step = 0;
-  Builder(Model& mm, Plan* p, int b) : m(mm), plan(p), B(b) {}
+  bool ragged = false;       // per-utterance lengths (Buf::LEN) mask the time axis
+  Builder(Model& mm, Plan* p, int b, bool rg = false) : m(mm), plan(p), B(b), ragged(rg) {}
   Buf alloc(size_t floats);
   void step(const std::string& name, Step s, const std::string& kernel = "");
   // emit an implicit-GEMM conv; pointers of `d` are taken from the Bufs
   struct ConvIO {
     Buf s0, s0b, s1, out, res, affx, affy, gate, partial, rowbias;
+    Buf rowlen, vlen;   // ragged batches (int32 arrays): output / s0-input valid time extents
   };
   void conv(const std::string& name, ConvDesc d, const Packed& p, const ConvIO& io, bool use_bias = true);
 };

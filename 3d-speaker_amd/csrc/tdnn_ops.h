@@ -10,8 +10,12 @@ hipError_t launch_attn_pool(const float* logit, int ldl, const float* x, int ldx
                             float* out, hipStream_t s);
 hipError_t launch_se_apply(const float* x, int ldx, const float* gate, int ldg, const float* res, int ldr, float* out,
                            int ldo, int B, int T, int C, hipStream_t s);
+// vlen (optional, ragged batches): valid frames per utterance
 hipError_t launch_cam_context(const float* x, int B, int T, int C, int ld, int seg, int nseg, float* out, int ldo,
-                              hipStream_t s);
-hipError_t launch_stats_pool(const float* x, int B, int T, int C, int ld, float* out, hipStream_t s);
+                              hipStream_t s, const int* vlen = nullptr);
+hipError_t launch_stats_pool(const float* x, int B, int T, int C, int ld, float* out, hipStream_t s,
+                             const int* vlen = nullptr);
+// out[b] = (in[b] + 2 pad - k) / stride + 1 (valid frames after a strided conv)
+hipError_t launch_derive_len(const int* in, int* out, int B, int pad, int k, int stride, hipStream_t s);
 
 }  // namespace spk

@@ -91,40 +91,50 @@ __global__ void se_apply_kernel(const float* __restrict__ x, int ldx, const floa
 }
 
 // ctx[b, s, c] = mean_T(x)[b, c] + mean over frames [100 s, min(100 s + 100, T)) of x[b, :, c]
+// (ragged batches: utterance b has vlen[b] valid frames; segments past them are written as 0)
 __global__ void cam_context_kernel(const float* __restrict__ x, int B, int T, int C, int ld, int seg, int nseg,
-                                   float* __restrict__ out, int ldo) {
+                                   float* __restrict__ out, int ldo, const int* __restrict__ vlen) {
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
        e += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(e % C), b = (int)(e / C);
+    const int Tb = vlen ? vlen[b] : T;
     const float* p = x + (size_t)b * T * ld + c;
     float tot = 0.f;
-    for (int t = 0; t < T; ++t) tot += p[(size_t)t * ld];
-    const float mean = tot / (float)T;
+    for (int t = 0; t < Tb; ++t) tot += p[(size_t)t * ld];
+    const float mean = tot / (float)Tb;
     for (int s = 0; s < nseg; ++s) {
-      const int t0 = s * seg, t1 = min(T, t0 + seg);
+      const int t0 = s * seg, t1 = min(Tb, t0 + seg);
       float a = 0.f;
       for (int t = t0; t < t1; ++t) a += p[(size_t)t * ld];
-      out[((size_t)b * nseg + s) * ldo + c] = mean + a / (float)(t1 - t0);
+      out[((size_t)b * nseg + s) * ldo + c] = t1 > t0 ? mean + a / (float)(t1 - t0) : 0.f;
     }
   }
 }
 
-__global__ void stats_pool_kernel(const float* __restrict__ x, int B, int T, int C, int ld, float* __restrict__ out) {
+__global__ void stats_pool_kernel(const float* __restrict__ x, int B, int T, int C, int ld, float* __restrict__ out,
+                                  const int* __restrict__ vlen) {
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
        e += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(e % C), b = (int)(e / C);
+    const int Tb = vlen ? vlen[b] : T;
     const float* p = x + (size_t)b * T * ld + c;
     float s = 0.f;
-    for (int t = 0; t < T; ++t) s += p[(size_t)t * ld];
-    const float mean = s / (float)T;
+    for (int t = 0; t < Tb; ++t) s += p[(size_t)t * ld];
+    const float mean = s / (float)Tb;
     float q = 0.f;
-    for (int t = 0; t < T; ++t) {
+    for (int t = 0; t < Tb; ++t) {
       const float d = p[(size_t)t * ld] - mean;
       q += d * d;
     }
     out[(size_t)b * 2 * C + c] = mean;
-    out[(size_t)b * 2 * C + C + c] = sqrtf(q / (float)(T - 1));
+    out[(size_t)b * 2 * C + C + c] = sqrtf(q / (float)(Tb - 1));
   }
+}
+
+// out[b] = (in[b] + 2 pad - k) / stride + 1: valid output frames of a strided conv
+__global__ void derive_len_kernel(const int* __restrict__ in, int* __restrict__ out, int B, int pad, int k, int stride) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) out[b] = (in[b] + 2 * pad - k) / stride + 1;
 }
 
 }  // namespace
@@ -155,14 +165,19 @@ hipError_t launch_se_apply(const float* x, int ldx, const float* gate, int ldg, 
 }
 
 hipError_t launch_cam_context(const float* x, int B, int T, int C, int ld, int seg, int nseg, float* out, int ldo,
-                              hipStream_t s) {
+                              hipStream_t s, const int* vlen) {
   hipLaunchKernelGGL(cam_context_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, seg, nseg,
-                     out, ldo);
+                     out, ldo, vlen);
   return hipGetLastError();
 }
 
-hipError_t launch_stats_pool(const float* x, int B, int T, int C, int ld, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(stats_pool_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, out);
+hipError_t launch_stats_pool(const float* x, int B, int T, int C, int ld, float* out, hipStream_t s, const int* vlen) {
+  hipLaunchKernelGGL(stats_pool_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, out, vlen);
+  return hipGetLastError();
+}
+
+hipError_t launch_derive_len(const int* in, int* out, int B, int pad, int k, int stride, hipStream_t s) {
+  hipLaunchKernelGGL(derive_len_kernel, dim3((B + 255) / 256), dim3(256), 0, s, in, out, B, pad, k, stride);
   return hipGetLastError();
 }
 

@@ -42,11 +42,17 @@ SYMBOLS = {
     'spk_version': (ctypes.c_int, []),
     'spk_last_error': (ctypes.c_char_p, []),
     'spk_fbank_f32': (ctypes.c_int, [_P, _P, ctypes.c_int32, _P, _P, ctypes.c_int32, ctypes.c_int32, _P]),
+    'spk_fbank_f32_padded': (ctypes.c_int, [_P, _P, ctypes.c_int32, _P, _P, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_int32, _P]),
     'spk_model_create': (ctypes.c_int, [ctypes.POINTER(spk_model_config_t), ctypes.POINTER(spk_weight_t),
                                         ctypes.c_int32, ctypes.POINTER(_P)]),
     'spk_model_destroy': (ctypes.c_int, [_P]),
     'spk_model_workspace_bytes': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_size_t)]),
     'spk_model_forward': (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_size_t, _P, _P]),
+    'spk_model_workspace_bytes_lengths': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                         ctypes.POINTER(ctypes.c_size_t)]),
+    'spk_model_forward_lengths': (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_size_t, _P,
+                                                 _P]),
     'spk_model_flops': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_double)]),
     'spk_model_plan_size': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
     'spk_model_plan_step': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p,
@@ -143,6 +149,32 @@ def fbank(wavs: torch.Tensor, n_mels: int = 80, mean_nor: bool = False, lengths=
     return out[0] if squeeze else out
 
 
+def fbank_padded(wavs: torch.Tensor, lengths, n_mels: int = 80, mean_nor: bool = False):
+    """Ragged Fbank written straight into a zero-padded [B, T_max, n_mels] batch: returns
+    (feats, frames) with ``frames`` a device int32 [B] tensor of valid frames per row, the
+    input of the models' ``forward(x, lengths=frames)`` (spk_fbank_f32_padded)."""
+    require_device_tensor(wavs, 'fbank_padded')
+    wavs = wavs.to(torch.float32).contiguous()
+    B, L = wavs.shape
+    dev = wavs.device
+    lens = [int(v) for v in lengths]
+    if len(lens) != B or max(lens) > L or min(lens) < 400:
+        raise HipError('fbank_padded: need B lengths in [400, padded length]')
+    frames = [num_frames(n) for n in lens]
+    tmax = max(frames)
+    frame_off = [0]
+    for f in frames:
+        frame_off.append(frame_off[-1] + f)
+    wav_off = [i * L for i in range(B + 1)]
+    offs = torch.tensor([wav_off, frame_off], dtype=torch.int64).to(dev, non_blocking=True)
+    feats = torch.empty((B, tmax, n_mels), dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _check(lib().spk_fbank_f32_padded(wavs.data_ptr(), offs[0].data_ptr(), B, feats.data_ptr(),
+                                          offs[1].data_ptr(), tmax, n_mels, int(bool(mean_nor)), _stream(dev)),
+               'spk_fbank_f32_padded')
+    return feats, torch.tensor(frames, dtype=torch.int32).to(dev, non_blocking=True)
+
+
 # ----------------------------------------------------------------------------- models
 class NativeModel:
     """One ``spk_model_t`` handle (folded + packed weights on one device)."""
@@ -223,7 +255,14 @@ class NativeModel:
                    'spk_model_forward_timed')
         return list(ms)
 
-    def forward(self, feats: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def workspace_bytes_lengths(self, B: int, T: int, ragged: bool) -> int:
+        n = ctypes.c_size_t()
+        _check(lib().spk_model_workspace_bytes_lengths(self.handle, B, T, int(ragged), ctypes.byref(n)),
+               'spk_model_workspace_bytes_lengths')
+        return n.value
+
+    def forward(self, feats: torch.Tensor, out: Optional[torch.Tensor] = None, lengths=None) -> torch.Tensor:
+        """``lengths`` (optional): valid frames per row (variable-length batch, CAM++)."""
         require_device_tensor(feats, 'embedding forward')
         if feats.device != self.device:
             raise HipError(f'model handle lives on {self.device}, input on {feats.device}')
@@ -231,16 +270,26 @@ class NativeModel:
             raise HipError(f'expected feats [B, T, F], got {tuple(feats.shape)}')
         feats = feats.to(torch.float32).contiguous()
         B, T, _ = feats.shape
+        if lengths is not None:
+            lengths = torch.as_tensor(lengths, dtype=torch.int32).to(self.device).contiguous()
+            if lengths.numel() != B:
+                raise HipError(f'lengths has {lengths.numel()} entries for a batch of {B}')
         with torch.cuda.device(self.device):
-            need = self.workspace_bytes(B, T)
+            need = self.workspace_bytes(B, T) if lengths is None else self.workspace_bytes_lengths(B, T, True)
             if self._ws is None or self._ws.numel() < need:
                 self._ws = None
                 self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
             if out is None:
                 out = torch.empty((B, self.embed_dim), dtype=torch.float32, device=self.device)
-            _check(lib().spk_model_forward(self.handle, feats.data_ptr(), B, T, self._ws.data_ptr(),
-                                           self._ws.numel(), out.data_ptr(), _stream(self.device)),
-                   'spk_model_forward')
+            if lengths is None:
+                _check(lib().spk_model_forward(self.handle, feats.data_ptr(), B, T, self._ws.data_ptr(),
+                                               self._ws.numel(), out.data_ptr(), _stream(self.device)),
+                       'spk_model_forward')
+            else:
+                _check(lib().spk_model_forward_lengths(self.handle, feats.data_ptr(), B, T, lengths.data_ptr(),
+                                                       self._ws.data_ptr(), self._ws.numel(), out.data_ptr(),
+                                                       _stream(self.device)),
+                       'spk_model_forward_lengths')
         return out
 
 
@@ -265,12 +314,12 @@ class HipModuleMixin:
             handles[key] = h
         return h
 
-    def _hip_forward(self, x: torch.Tensor) -> torch.Tensor:
+    def _hip_forward(self, x: torch.Tensor, lengths=None) -> torch.Tensor:
         require_device_tensor(x, type(self).__name__ + '.forward')
         if self.training:
             raise HipError(f'{type(self).__name__}: the MI355X path is inference-only; call .eval()')
         dev = x.device if x.device.index is not None else torch.device('cuda', torch.cuda.current_device())
-        return self._hip_handle(dev).forward(x)
+        return self._hip_handle(dev).forward(x, lengths=lengths)
 
     def _apply(self, fn, *args, **kwargs):
         self._hip_reset()

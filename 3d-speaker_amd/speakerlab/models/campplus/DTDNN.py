@@ -71,6 +71,10 @@ class CAMPPlus(_hip.HipModuleMixin, nn.Module):
     def _hip_config(self):
         return dict(feat_dim=self.feat_dim, embed_dim=self.embedding_size)
 
-    def forward(self, x):
-        """x: [B, T, feat_dim] on a ROCm device -> [B, embedding_size]."""
-        return self._hip_forward(x)
+    def forward(self, x, lengths=None):
+        """x: [B, T, feat_dim] on a ROCm device -> [B, embedding_size].
+
+        ``lengths`` (extension, optional): valid frames of each row for a variable-length
+        batch (e.g. from ``speakerlab._hip.fbank_padded``); row b then gets exactly the
+        embedding of its first lengths[b] frames on their own."""
+        return self._hip_forward(x, lengths=lengths)

@@ -84,6 +84,12 @@ const char* spk_last_error(void);
 int spk_fbank_f32(const float* wav, const int64_t* wav_offsets, int32_t n_utt, float* feats,
                   const int64_t* frame_offsets, int32_t n_mels, int32_t mean_nor, void* stream);
 
+/* Same, written as a zero-padded batch [n_utt, t_max, n_mels]: utterance u at rows
+ * [u * t_max, u * t_max + frames_u) (frames_u from frame_offsets), its remaining rows 0.
+ * The input of spk_model_forward_lengths for variable-length batches. */
+int spk_fbank_f32_padded(const float* wav, const int64_t* wav_offsets, int32_t n_utt, float* feats,
+                         const int64_t* frame_offsets, int32_t t_max, int32_t n_mels, int32_t mean_nor, void* stream);
+
 /* Build a handle on the CURRENT HIP device: folds BatchNorm into conv weights, packs them
  * for the kernels and uploads them (synchronous, once per model). */
 int spk_model_create(const spk_model_config_t* cfg, const spk_weight_t* weights, int32_t n_weights,
@@ -96,6 +102,16 @@ int spk_model_workspace_bytes(spk_model_t* model, int32_t B, int32_t T, size_t* 
 /* feats: device [B, T, feat_dim] float32; emb_out: device [B, embed_dim] float32. */
 int spk_model_forward(spk_model_t* model, const float* feats, int32_t B, int32_t T, void* workspace,
                       size_t workspace_bytes, float* emb_out, void* stream);
+
+/* Variable-length batch (CAM++): feats is [B, T, feat_dim] with
+ * utterance b occupying frames [0, lengths[b]) (lengths: DEVICE int32 [B], 2 <= lengths[b]
+ * <= T; frames past it are ignored).  Every embedding equals the forward of that utterance
+ * alone (no padding enters the computation).  lengths == NULL is spk_model_forward.
+ * Replaces running the reference model (DTDNN.py:111-115) once per utterance.
+ * Other architectures return SPK_E_UNSUPPORTED for a non-NULL lengths. */
+int spk_model_workspace_bytes_lengths(spk_model_t* model, int32_t B, int32_t T, int32_t ragged, size_t* bytes);
+int spk_model_forward_lengths(spk_model_t* model, const float* feats, int32_t B, int32_t T, const int32_t* lengths,
+                              void* workspace, size_t workspace_bytes, float* emb_out, void* stream);
 
 /* Algorithmic FLOPs per utterance of T frames (2 x conv/linear MACs). */
 int spk_model_flops(spk_model_t* model, int32_t T, double* flops);

@@ -46,7 +46,7 @@ static float epilogue(const ConvDesc& d, int m, int n, float v) {
     const int wo = m % d.Wo, img = m / (d.Wo * d.Ho);
     v *= d.gate[((size_t)img * d.gate_nseg + wo / d.gate_seg) * d.gate_ld + n];
   }
-  return v;
+  return row_masked(d, m) ? 0.f : v;
 }
 
 hipError_t launch_conv(const ConvDesc& d, hipStream_t) {
@@ -67,7 +67,7 @@ hipError_t launch_conv(const ConvDesc& d, hipStream_t) {
           hi = hi < 0 ? -hi : (hi >= d.s0.H ? 2 * d.s0.H - 2 - hi : hi);
           wi = wi < 0 ? -wi : (wi >= d.s0.W ? 2 * d.s0.W - 2 - wi : wi);
         }
-        if (hi >= 0 && hi < d.s0.H && wi >= 0 && wi < d.s0.W) {
+        if (hi >= 0 && hi < d.s0.H && wi >= 0 && wi < d.s0.W && (!d.s0.vlen || wi < d.s0.vlen[img])) {
           const size_t pix = (size_t)(img * d.s0.H + hi) * d.s0.W + wi;
           v = d.s0.p[pix * d.s0.ld + c];
           if (d.s0.p2) v += d.s0.p2[pix * d.s0.ld2 + c];
@@ -96,8 +96,9 @@ std::string conv_kernel_name(const ConvDesc&) { return "emu_conv"; }
 hipError_t launch_split_f16(const float*, uint16_t*, uint16_t*, size_t, hipStream_t) { return hipSuccess; }
 
 hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const float* w, const float* bias, int cout,
-                               int act, int wstride, float* out, int ldo, hipStream_t) {
-  for (int b = 0; b < B; ++b)
+                               int act, int wstride, float* out, int ldo, hipStream_t, const int* vlen) {
+  for (int b = 0; b < B; ++b) {
+    const int Tb = vlen ? vlen[b] : T;
     for (int f = 0; f < F; ++f)
       for (int t = 0; t < T; ++t)
         for (int c = 0; c < cout; ++c) {
@@ -105,11 +106,12 @@ hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const fl
           for (int dy = 0; dy < 3; ++dy)
             for (int dx = 0; dx < 3; ++dx) {
               const int ff = f + dy - 1, tt = t + dx - 1;
-              if (ff >= 0 && ff < F && tt >= 0 && tt < T) acc += (double)feats[((size_t)b * T + tt) * F + ff] * w[c * wstride + dy * 3 + dx];
+              if (ff >= 0 && ff < F && tt >= 0 && tt < Tb) acc += (double)feats[((size_t)b * T + tt) * F + ff] * w[c * wstride + dy * 3 + dx];
             }
           float v = (float)acc + bias[c];
-          out[(((size_t)b * F + f) * T + t) * ldo + c] = act == ACT_RELU ? std::fmax(v, 0.f) : v;
+          out[(((size_t)b * F + f) * T + t) * ldo + c] = t >= Tb ? 0.f : (act == ACT_RELU ? std::fmax(v, 0.f) : v);
         }
+  }
   return hipSuccess;
 }
 
@@ -133,7 +135,7 @@ hipError_t launch_tstp(const float* x, int B, int H, int W, int C, int ld, float
 }
 
 hipError_t launch_fbank(const float*, const int64_t*, int, float*, const int64_t*, int, int, const FbankTables*,
-                        hipStream_t) {
+                        hipStream_t, int) {
   return hipErrorNotSupported;
 }
 
@@ -222,30 +224,38 @@ hipError_t launch_se_apply(const float* x, int ldx, const float* g, int ldg, con
   return hipSuccess;
 }
 hipError_t launch_cam_context(const float* x, int B, int T, int C, int ld, int seg, int nseg, float* out, int ldo,
-                              hipStream_t) {
-  for (int b = 0; b < B; ++b)
+                              hipStream_t, const int* vlen) {
+  for (int b = 0; b < B; ++b) {
+    const int Tb = vlen ? vlen[b] : T;
     for (int c = 0; c < C; ++c) {
       double tot = 0;
-      for (int t = 0; t < T; ++t) tot += x[((size_t)b * T + t) * ld + c];
+      for (int t = 0; t < Tb; ++t) tot += x[((size_t)b * T + t) * ld + c];
       for (int s = 0; s < nseg; ++s) {
-        const int t0 = s * seg, t1 = std::min(T, t0 + seg);
+        const int t0 = s * seg, t1 = std::min(Tb, t0 + seg);
         double a = 0;
         for (int t = t0; t < t1; ++t) a += x[((size_t)b * T + t) * ld + c];
-        out[((size_t)b * nseg + s) * ldo + c] = (float)(tot / T + a / (t1 - t0));
+        out[((size_t)b * nseg + s) * ldo + c] = t1 > t0 ? (float)(tot / Tb + a / (t1 - t0)) : 0.f;
       }
     }
+  }
   return hipSuccess;
 }
-hipError_t launch_stats_pool(const float* x, int B, int T, int C, int ld, float* out, hipStream_t) {
-  for (int b = 0; b < B; ++b)
+hipError_t launch_stats_pool(const float* x, int B, int T, int C, int ld, float* out, hipStream_t, const int* vlen) {
+  for (int b = 0; b < B; ++b) {
+    const int Tb = vlen ? vlen[b] : T;
     for (int c = 0; c < C; ++c) {
       double s = 0, q = 0;
-      for (int t = 0; t < T; ++t) s += x[((size_t)b * T + t) * ld + c];
-      const double mean = s / T;
-      for (int t = 0; t < T; ++t) { const double d = x[((size_t)b * T + t) * ld + c] - mean; q += d * d; }
+      for (int t = 0; t < Tb; ++t) s += x[((size_t)b * T + t) * ld + c];
+      const double mean = s / Tb;
+      for (int t = 0; t < Tb; ++t) { const double d = x[((size_t)b * T + t) * ld + c] - mean; q += d * d; }
       out[(size_t)b * 2 * C + c] = (float)mean;
-      out[(size_t)b * 2 * C + C + c] = (float)std::sqrt(q / (T - 1));
+      out[(size_t)b * 2 * C + C + c] = (float)std::sqrt(q / (Tb - 1));
     }
+  }
+  return hipSuccess;
+}
+hipError_t launch_derive_len(const int* in, int* out, int B, int pad, int k, int stride, hipStream_t) {
+  for (int b = 0; b < B; ++b) out[b] = (in[b] + 2 * pad - k) / stride + 1;
   return hipSuccess;
 }
 }  // namespace spk

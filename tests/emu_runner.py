@@ -58,15 +58,18 @@ class EmuModel:
         self.handle = ctypes.c_void_p()
         _check(lib().spk_model_create(ctypes.byref(c), ws, len(sd), ctypes.byref(self.handle)), 'create')
 
-    def __call__(self, feats):
+    def __call__(self, feats, lengths=None):
         feats = feats.float().contiguous()
         B, T, _ = feats.shape
         n = ctypes.c_size_t()
-        _check(lib().spk_model_workspace_bytes(self.handle, B, T, ctypes.byref(n)), 'workspace')
+        _check(lib().spk_model_workspace_bytes_lengths(self.handle, B, T, int(lengths is not None), ctypes.byref(n)),
+               'workspace')
         ws = torch.zeros(max(n.value, 256), dtype=torch.uint8)
         out = torch.empty(B, self.embed_dim)
-        _check(lib().spk_model_forward(self.handle, feats.data_ptr(), B, T, ws.data_ptr(), ws.numel(),
-                                       out.data_ptr(), None), 'forward')
+        lens = None if lengths is None else torch.as_tensor(lengths, dtype=torch.int32).contiguous()
+        _check(lib().spk_model_forward_lengths(self.handle, feats.data_ptr(), B, T,
+                                               None if lens is None else lens.data_ptr(), ws.data_ptr(), ws.numel(),
+                                               out.data_ptr(), None), 'forward')
         return out
 
     def plan(self, B, T):

@@ -52,3 +52,23 @@ def test_flops_attributed_per_step(arch):
     for name, f, kern in steps:
         if kern.startswith(('conv_gemm', 'conv3x3')):
             assert f > 0, (name, kern)
+
+
+@pytest.mark.parametrize('arch', ['campplus', 'campplus_192'])
+def test_emulated_ragged_campplus_matches_per_utterance(arch):
+    """Variable-length batch (config C3): row b of a padded batch with lengths[b] valid
+    frames equals the reference forward of that utterance alone; the padding frames hold
+    garbage that must not leak in."""
+    g = helpers.golden(arch)
+    m = helpers.loaded_module(arch)
+    sd = helpers.state_dict(arch, torch.float64)
+    full = torch.from_numpy(g['feats0'][:3]).float()            # 3 x 198 frames
+    lengths = [198, 120, 161]
+    feats = full.clone()
+    gen = torch.Generator().manual_seed(0)
+    for b, n in enumerate(lengths):
+        feats[b, n:] = 50 * torch.randn(198 - n, full.shape[2], generator=gen)
+    emb = EmuModel(m)(feats, lengths).numpy()
+    for b, n in enumerate(lengths):
+        ref = models_ref.forward(arch, sd, full[b:b + 1, :n].double()).numpy()
+        assert helpers.rel_err(emb[b:b + 1], ref).max() < 1e-5, (b, n)

@@ -6,7 +6,8 @@ import pytest
 import torch
 
 import helpers
-from oracle import models_ref
+from oracle import fbank_ref, models_ref
+from speakerlab import _hip
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
@@ -74,3 +75,49 @@ def test_weight_reload_invalidates_native_handle():
         m.load_state_dict(sd)
         b = m(x).cpu().numpy()
     np.testing.assert_allclose(b - a, 1.0, atol=1e-4)
+
+
+@pytest.mark.parametrize('arch', ['campplus', 'campplus_192'])
+def test_ragged_campplus_matches_per_utterance(arch):
+    """Config C3: a variable-length batch gives every row the embedding of that utterance
+    alone (padding frames hold garbage that must not leak in)."""
+    g = helpers.golden(arch)
+    sd = helpers.state_dict(arch, torch.float64)
+    full = torch.from_numpy(g['feats0'][:3]).float()
+    lengths = [198, 120, 161]
+    feats = full.clone()
+    gen = torch.Generator().manual_seed(0)
+    for b, n in enumerate(lengths):
+        feats[b, n:] = 50 * torch.randn(198 - n, full.shape[2], generator=gen)
+    m = gpu_module(arch)
+    with torch.no_grad():
+        emb = m(feats.cuda(), lengths=torch.tensor(lengths, dtype=torch.int32)).cpu().numpy()
+    for b, n in enumerate(lengths):
+        ref = models_ref.forward(arch, sd, full[b:b + 1, :n].double()).numpy()
+        assert helpers.rel_err(emb[b:b + 1], ref).max() < TOL, (b, n)
+
+
+def test_ragged_wav_batch_end_to_end():
+    """1-5 s utterances: padded GPU Fbank + ragged CAM++ forward == per-utterance oracle."""
+    from speakerlab.utils import synthetic
+    lens = [16000, 80000, 33333, 47000, 16400]
+    L = max(lens)
+    wavs = np.zeros((len(lens), L), np.float32)
+    for i, n in enumerate(lens):
+        wavs[i, :n] = synthetic.synth_wav(n, seed=500 + i)
+    feats, frames = _hip.fbank_padded(torch.from_numpy(wavs).cuda(), lens, 80, mean_nor=True)
+    m = gpu_module('campplus')
+    with torch.no_grad():
+        emb = m(feats, lengths=frames).cpu().numpy()
+    sd = helpers.state_dict('campplus', torch.float64)
+    for i, n in enumerate(lens):
+        f = torch.from_numpy(fbank_ref.fbank(wavs[i, :n], 80, True))[None]
+        ref = models_ref.forward('campplus', sd, f).numpy()
+        assert helpers.rel_err(emb[i:i + 1], ref).max() < 5e-4, i   # incl. fp32 Fbank noise
+
+
+def test_ragged_unsupported_arch_raises():
+    h = gpu_module('eres2netv2')._hip_handle(torch.device('cuda', 0))
+    x = torch.zeros(2, 98, 80, device='cuda')
+    with pytest.raises(_hip.HipError):
+        h.forward(x, lengths=torch.tensor([98, 50], dtype=torch.int32))
