@@ -148,7 +148,7 @@ pw_gemm_x3_kernel(const ConvDesc d) {
         if (m >= M) continue;
         float v = apply_act(acc[r] + accx[r] * (1.0f / 2048.0f) + bias + res[r], d.act);
         if (d.post_scale) v = v * ps + pt;
-        d.out[(size_t)m * d.ldo + n] = apply_act(v, d.act2);
+        d.out[(size_t)m * d.ldo + n] = row_masked(d, m) ? 0.f : apply_act(v, d.act2);
       }
     }
   };
@@ -217,7 +217,7 @@ bool pw_supported(const ConvDesc& d) {
                          ? true
                          : (d.s1.kh == 1 && d.s1.kw == 1 && d.s1.sh == 1 && d.s1.sw == 1 && d.s1.ph == 0 &&
                             d.s1.pw == 0 && d.s1.cin % 4 == 0 && d.s1.ld % 4 == 0);
-  return d.wh && d.wl && !d.rowlen && !a.vlen && a.kh == 1 && a.kw == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0 && !a.reflect &&
+  return d.wh && d.wl && !a.vlen && a.kh == 1 && a.kw == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0 && !a.reflect &&
          !a.pre_scale && !a.p2 && a.ld2 == 0 && s1_ok && (d.Kp == 64 || d.Kp == 128) && d.N <= 256 &&
          d.N % 4 == 0 && !d.affx && !d.gate && !d.rowbias && d.ksplit == 1 && a.cin % 4 == 0 &&
          a.H == d.Ho && a.W == d.Wo && d.nimg * d.Ho * d.Wo >= 65536;

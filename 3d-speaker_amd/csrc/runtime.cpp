@@ -2,6 +2,7 @@
 #include "runtime.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "fbank.h"
@@ -230,6 +231,14 @@ int hip_check(hipError_t e, const char* what) {
   return SPK_E_HIP;
 }
 
+}  // namespace
+
+spk::Plan::~Plan() {
+  for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+}
+
+namespace {
+
 Plan* get_plan(spk_model_t* h, int B, int T, bool ragged = false) {
   std::lock_guard<std::mutex> lk(h->m.mu);
   auto key = std::make_pair(B, ragged ? -T : T);
@@ -246,7 +255,18 @@ Plan* get_plan(spk_model_t* h, int B, int T, bool ragged = false) {
     case SPK_ARCH_CAMPPLUS: build_campplus(b, T); break;
     default: throw SpkError(SPK_E_UNSUPPORTED, "unknown arch");
   }
-  plan->ws_bytes = b.ws;
+  // staging regions for graph replay (input features, per-utterance lengths, embeddings)
+  plan->in_bytes = (size_t)B * T * h->m.cfg.feat_dim * sizeof(float);
+  plan->out_bytes = (size_t)B * h->m.cfg.embed_dim * sizeof(float);
+  plan->len_bytes = ragged ? (size_t)B * sizeof(int32_t) : 0;
+  size_t ws = (b.ws + 255) / 256 * 256;
+  plan->stage_in = ws;
+  ws += (plan->in_bytes + 255) / 256 * 256;
+  plan->stage_out = ws;
+  ws += (plan->out_bytes + 255) / 256 * 256;
+  plan->stage_len = ws;
+  ws += (plan->len_bytes + 255) / 256 * 256;
+  plan->ws_bytes = ws;
   Plan* p = plan.get();
   h->m.plans.emplace(key, std::move(plan));
   return p;
@@ -412,6 +432,67 @@ int spk_model_flops(spk_model_t* model, int32_t T, double* flops) {
   });
 }
 
+// SPK_GRAPH=0 launches every step directly instead of replaying a captured hipGraph
+static bool use_graphs() {
+  static const bool on = [] {
+    const char* e = std::getenv("SPK_GRAPH");
+    return !(e && std::string(e) == "0");
+  }();
+  return on;
+}
+
+// Replay the plan as one hipGraph: inputs are copied into the workspace's staging regions,
+// the graph (captured once per workspace address on a private stream) runs on the caller's
+// stream, and the embeddings are copied out.  Removes the per-kernel launch cost (CAM++ has
+// ~280 launches per forward).
+static int run_graph(const char* fn, spk_model_t* model, Plan* plan, const float* feats, const int32_t* lengths,
+                     char* ws, float* emb_out, hipStream_t stream) {
+  char* in_s = ws + plan->stage_in;
+  char* out_s = ws + plan->stage_out;
+  char* len_s = ws + plan->stage_len;
+  if (int rc = hip_check(hipMemcpyAsync(in_s, feats, plan->in_bytes, hipMemcpyDeviceToDevice, stream), "stage in"))
+    return rc;
+  if (lengths && plan->len_bytes)
+    if (int rc = hip_check(hipMemcpyAsync(len_s, lengths, plan->len_bytes, hipMemcpyDeviceToDevice, stream),
+                           "stage lengths"))
+      return rc;
+  hipGraphExec_t exec = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(model->m.mu);
+    auto it = plan->graphs.find(ws);
+    if (it != plan->graphs.end()) exec = it->second;
+  }
+  if (!exec) {
+    hipStream_t cap = nullptr;
+    if (int rc = hip_check(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking), "hipStreamCreate")) return rc;
+    Ctx c{ws, reinterpret_cast<const float*>(in_s), reinterpret_cast<float*>(out_s), cap,
+          lengths ? reinterpret_cast<const int*>(len_s) : nullptr};
+    hipGraph_t graph = nullptr;
+    int rc = hip_check(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+    for (size_t i = 0; rc == SPK_OK && i < plan->steps.size(); ++i) {
+      hipError_t e = plan->steps[i](c);
+      if (e != hipSuccess) {
+        set_error(std::string(fn) + ": capture of step '" + plan->names[i] + "': " + hipGetErrorString(e));
+        rc = SPK_E_HIP;
+      }
+    }
+    const hipError_t ee = hipStreamEndCapture(cap, &graph);
+    if (rc == SPK_OK) rc = hip_check(ee, "hipStreamEndCapture");
+    if (rc == SPK_OK) rc = hip_check(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0), "hipGraphInstantiate");
+    if (graph) (void)hipGraphDestroy(graph);
+    (void)hipStreamDestroy(cap);
+    if (rc != SPK_OK) return rc;
+    std::lock_guard<std::mutex> lk(model->m.mu);
+    auto ins = plan->graphs.emplace(ws, exec);
+    if (!ins.second) {   // another thread captured the same one first
+      (void)hipGraphExecDestroy(exec);
+      exec = ins.first->second;
+    }
+  }
+  if (int rc = hip_check(hipGraphLaunch(exec, stream), "hipGraphLaunch")) return rc;
+  return hip_check(hipMemcpyAsync(emb_out, out_s, plan->out_bytes, hipMemcpyDeviceToDevice, stream), "stage out");
+}
+
 static int run_forward(const char* fn, spk_model_t* model, const float* feats, int32_t B, int32_t T,
                        const int32_t* lengths, void* workspace, size_t workspace_bytes, float* emb_out, void* stream) {
   if (!model || !feats || !emb_out || B <= 0 || T <= 0) {
@@ -429,6 +510,9 @@ static int run_forward(const char* fn, spk_model_t* model, const float* feats, i
     set_error(std::string(fn) + ": workspace too small (need " + std::to_string(plan->ws_bytes) + " bytes)");
     return SPK_E_WORKSPACE;
   }
+  if (use_graphs())
+    return run_graph(fn, model, plan, feats, lengths, reinterpret_cast<char*>(workspace), emb_out,
+                     reinterpret_cast<hipStream_t>(stream));
   Ctx c{reinterpret_cast<char*>(workspace), feats, emb_out, reinterpret_cast<hipStream_t>(stream), lengths};
   for (size_t i = 0; i < plan->steps.size(); ++i) {
     hipError_t e = plan->steps[i](c);

@@ -56,6 +56,12 @@ struct Plan {
   std::vector<std::string> kernels; // kernel instantiation each step launches
   std::vector<double> flops;        // algorithmic FLOPs of the step (whole batch)
   size_t ws_bytes = 0;
+  // hipGraph replay: the plan's launches captured once per workspace address, reading the
+  // input / lengths from and writing the output to staging regions of the workspace
+  size_t stage_in = 0, stage_out = 0, stage_len = 0;   // byte offsets in the workspace
+  size_t in_bytes = 0, out_bytes = 0, len_bytes = 0;
+  std::map<const void*, hipGraphExec_t> graphs;
+  ~Plan();
 };
 
 // Logical -> physical channel map of a channels-last tensor (zero-padded slices).

@@ -18,6 +18,7 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
+        os.environ['SPK_GRAPH'] = '0'   # launches are emulated one by one (no graph replay)
         subprocess.run(['make', '-s', '-C', EMU_DIR], check=True)
         h = ctypes.CDLL(os.path.join(EMU_DIR, 'libspk_emu.so'))
         for name, (res, args) in _hip.SYMBOLS.items():
