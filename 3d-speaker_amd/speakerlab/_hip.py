@@ -62,6 +62,9 @@ SYMBOLS = {
                                                _P, ctypes.c_int32]),
     'spk_cosine_affinity': (ctypes.c_int, [_P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int32, _P,
                                            ctypes.c_int64, _P]),
+    'spk_spectral_laplacian': (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, _P, ctypes.c_int64,
+                                              _P, ctypes.c_size_t, _P]),
+    'spk_symmetric_eig': (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int64, _P, _P]),
 }
 
 _lib = None
@@ -342,3 +345,31 @@ def cosine_affinity(a: torch.Tensor, b: Optional[torch.Tensor] = None, out: Opti
         _check(lib().spk_cosine_affinity(a.data_ptr(), a.shape[0], b.data_ptr(), b.shape[0], a.shape[1],
                                          out.data_ptr(), out.stride(0), _stream(a.device)), 'spk_cosine_affinity')
     return out
+
+
+def spectral_laplacian(S: torch.Tensor, n_elems: int) -> torch.Tensor:
+    """p-pruned, symmetrised unnormalised Laplacian of an N x N affinity (device)."""
+    require_device_tensor(S, 'spectral_laplacian')
+    S = S.to(torch.float32).contiguous()
+    N = S.shape[0]
+    L = torch.empty_like(S)
+    ws = torch.empty(N * N, dtype=torch.float32, device=S.device)
+    with torch.cuda.device(S.device):
+        _check(lib().spk_spectral_laplacian(S.data_ptr(), N, S.stride(0), max(0, int(n_elems)), L.data_ptr(),
+                                            L.stride(0), ws.data_ptr(), ws.numel() * 4, _stream(S.device)),
+               'spk_spectral_laplacian')
+    return L
+
+
+def symmetric_eig(A: torch.Tensor):
+    """(eigenvalues ascending [N], eigenvectors as ROWS [N, N]) of a symmetric device matrix;
+    A is overwritten."""
+    require_device_tensor(A, 'symmetric_eig')
+    if A.dtype != torch.float32 or not A.is_contiguous():
+        raise HipError('symmetric_eig: float32 contiguous matrix expected')
+    N = A.shape[0]
+    w = torch.empty(N, dtype=torch.float32, device=A.device)
+    with torch.cuda.device(A.device):
+        _check(lib().spk_symmetric_eig(A.data_ptr(), N, A.stride(0), w.data_ptr(), _stream(A.device)),
+               'spk_symmetric_eig')
+    return w, A

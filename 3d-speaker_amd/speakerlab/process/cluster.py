@@ -79,17 +79,60 @@ def spectral_labels(S: np.ndarray, min_num_spks=1, max_num_spks=10, pval=0.02, m
     return labels
 
 
+_solver_warm = False
+
+
+def _warm_solver():
+    """rocBLAS / rocSOLVER load their kernels on first use (~1 s): pay it at construction."""
+    global _solver_warm
+    if _solver_warm:
+        return
+    import torch
+    if torch.cuda.is_available():
+        from speakerlab import _hip
+        _hip.symmetric_eig(torch.eye(8, device='cuda'))
+        _solver_warm = True
+
+
+def spectral_labels_gpu(X, min_num_spks=1, max_num_spks=10, pval=0.02, min_pnum=6, oracle_num=None):
+    """The same steps with the N x N work on the GPU: cosine affinity (MFMA), p-pruning +
+    symmetrisation + Laplacian (csrc/spectral.hip), all eigenpairs by rocSOLVER ssyevd (in
+    place of ARPACK eigsh 'SM'); eigen-gap and k-means on the host as in the reference."""
+    import torch
+    from sklearn.cluster._kmeans import k_means
+    from speakerlab import _hip
+    if not torch.cuda.is_available():
+        raise _hip.HipError('spectral clustering runs on the ROCm device; none is available')
+    t = torch.as_tensor(np.ascontiguousarray(X, dtype=np.float32)).cuda()
+    n = t.shape[0]
+    S = _hip.cosine_affinity(t)
+    n_elems = min(int((1 - pval) * n), n - min_pnum)
+    L = _hip.spectral_laplacian(S, n_elems)
+    del S
+    kk = min(max_num_spks + 1, n)
+    w, V = _hip.symmetric_eig(L)
+    lambdas = w[:kk].cpu().numpy()
+    if oracle_num is not None:
+        k = oracle_num
+    else:
+        gaps = np.diff(lambdas[min_num_spks - 1:max_num_spks + 1].astype(np.float64))
+        k = int(np.argmax(gaps)) + min_num_spks
+    emb = V[:k].t().contiguous().cpu().numpy()
+    _, labels, _ = k_means(emb, k)
+    return labels
+
+
 class SpectralCluster:
     def __init__(self, min_num_spks=1, max_num_spks=10, pval=0.02, min_pnum=6, oracle_num=None):
         self.min_num_spks, self.max_num_spks = min_num_spks, max_num_spks
         self.min_pnum, self.pval, self.k = min_pnum, pval, oracle_num
+        _warm_solver()
 
     def __call__(self, X, **kwargs):
         pval = kwargs.get('pval', None)
         oracle = kwargs.get('speaker_num', None)
-        return spectral_labels(cosine_affinity(X), self.min_num_spks, self.max_num_spks,
-                               self.pval if pval is None else pval, self.min_pnum,
-                               self.k if oracle is None else oracle)
+        return spectral_labels_gpu(X, self.min_num_spks, self.max_num_spks, self.pval if pval is None else pval,
+                                   self.min_pnum, self.k if oracle is None else oracle)
 
 
 class UmapHdbscan:

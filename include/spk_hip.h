@@ -133,6 +133,20 @@ int spk_model_forward_timed(spk_model_t* model, const float* feats, int32_t B, i
 int spk_cosine_affinity(const float* Ea, int64_t Na, const float* Eb, int64_t Nb, int32_t E, float* out,
                         int64_t ldo, void* stream);
 
+/* Spectral clustering preparation (reference cluster.py SpectralCluster.p_pruning :64-77
+ * and get_laplacian :79-84): S is the N x N cosine affinity (row stride lds); every row's
+ * n_elems smallest entries are zeroed (ties at the threshold lowest index first), the
+ * result symmetrised, its diagonal zeroed, and L = diag(row |sums|) - M written to L (row
+ * stride ldl).  workspace: N*N floats (device). */
+int spk_spectral_laplacian(const float* S, int64_t N, int64_t lds, int32_t n_elems, float* L, int64_t ldl,
+                           void* workspace, size_t workspace_bytes, void* stream);
+
+/* All eigenpairs of a symmetric N x N matrix (rocSOLVER ssyevd; replaces ARPACK eigsh in
+ * cluster.py:88-89): eigenvalues ascending into w (device, N), eigenvector k overwrites row
+ * k of A (row-major, stride lda).  Synchronises the stream. */
+int spk_symmetric_eig(float* A, int64_t N, int64_t lda, float* w, void* stream);
+
+
 #ifdef __cplusplus
 }
 #endif
