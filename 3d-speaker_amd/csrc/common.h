@@ -71,6 +71,20 @@ __host__ __device__ inline bool row_masked(const ConvDesc& d, int m) {
   return wo >= d.rowlen[img];
 }
 
+// The conv GEMM's buffer-resource loader (conv_loader.h BufALoader) applies: zero padding,
+// s0.cin >= 32 (one tap boundary per 32-deep K-tile), at most 30 taps, and every operand
+// byte a block of `bm` rows can touch within 2 GiB of its first image.  Otherwise the
+// generic loader runs, which exists for the plain and the addend (ADD) forms only.
+inline bool conv_buf_loader_ok(const ConvDesc& d, int bm) {
+  if (d.s0.reflect || d.s0.cin < 32 || d.s0.kh * d.s0.kw > 30) return false;
+  const double span = (double)(bm / (d.Ho * d.Wo) + 2);
+  const double lim = 0x7FFFFFF0 - 64;
+  if (span * d.s0.H * d.s0.W * d.s0.ld * 4.0 > lim) return false;
+  if (d.s0.p2 && span * d.s0.H * d.s0.W * d.s0.ld2 * 4.0 > lim) return false;
+  if (d.s1.p && span * d.s1.H * d.s1.W * d.s1.ld * 4.0 > lim) return false;
+  return (double)d.N * d.Kp * 2.0 < lim;
+}
+
 hipError_t launch_conv(const ConvDesc& d, hipStream_t s);
 bool conv_use_x3();   // fp16x3 split-precision MFMA path (default; SPK_CONV_MFMA=f32 selects exact fp32 MFMA)
 std::string conv_kernel_name(const ConvDesc& d);

@@ -17,6 +17,7 @@
 // LDS rows are padded to 20 floats, which makes those b128 reads bank-conflict free.
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #include "common.h"
 #include "conv_epilogue.h"
@@ -194,7 +195,7 @@ struct X3Cfg {
   static constexpr int LDS_FLOATS = STAGE > LDS_EPI ? STAGE : LDS_EPI;
 };
 
-template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE>
+template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE, bool BUF>
 __global__ void __launch_bounds__(64 * WM * WN, 1)
 conv_gemm_x3_kernel(const ConvDesc d) {
   using C = X3Cfg<BM, BN, WM, WN>;
@@ -218,42 +219,45 @@ conv_gemm_x3_kernel(const ConvDesc d) {
   const int kt0 = blockIdx.z * per;
   const int kt1 = min(nkt_all, kt0 + per);
 
-  // ---- A: asynchronous implicit-im2col loader (conv_loader.h)
+  // ---- A: asynchronous implicit-im2col loader (conv_loader.h): the buffer-resource form
+  // wherever the layer allows it (BUF), else the generic one (reflect padding, cin < 32)
   const int kq = tid % C::QPR, row0 = tid / C::QPR;
-  using AL = ALoader<AROWS, RPP, BK, S1, ADD, PRE>;
+  using AL = typename std::conditional<BUF, BufALoader<AROWS, RPP, BK, S1, ADD, PRE>,
+                                       ALoader<AROWS, RPP, BK, S1, ADD, PRE>>::type;
   AL al;
   al.init(d, m0, row0, kq, kt0);
-  // ---- B chunk geometry: chunk cb = (plane, quarter) of a 32-half weight row
-  const int cb = tid % C::CPR, brow0 = tid / C::CPR;
-  const uint16_t* bsrc = (cb >> 2) ? d.wl : d.wh;
-  const int bq = cb & 3;
+  // ---- B chunk geometry: the first half of the block loads the hi plane, the second the
+  // lo plane (wave-uniform, so each wave reads through one buffer resource); a thread owns
+  // one 16-B quarter of a 32-half weight row.  Rows past N read zeros (offset past range).
+  const int plane = __builtin_amdgcn_readfirstlane(tid / (C::NT / 2));
+  const int bq = tid & 3, brow0 = (tid % (C::NT / 2)) >> 2;
+  const __amdgpu_buffer_rsrc_t brs = make_rsrc(plane ? d.wl : d.wh);
+  uint32_t boff[C::BROWS];
+#pragma unroll
+  for (int r = 0; r < C::BROWS; ++r) {
+    const int nr = brow0 + C::RPPB * r;
+    boff[r] = (nr < BN && n0 + nr < d.N) ? ((uint32_t)(n0 + nr) * d.Kp + bq * 8) * 2u : BUF_OOB;
+  }
 
   // two register sets: the loads of K-tile kt+2 are issued before the MFMAs of tile kt, so
   // every load has two K-steps of compute to land (prefetch distance 2, LDS double buffer)
   struct Set {
     typename AL::Slot a;
     u32x4 b[C::BROWS];
-    unsigned bok;
   };
   Set set0, set1;
 
   auto load_tile = [&](int kt, Set& st) {
     al.load(d, st.a);
-    st.bok = 0;
+    const int koff = __builtin_amdgcn_readfirstlane(kt * BK * 2);   // uniform: no waterfall (T20)
 #pragma unroll
-    for (int r = 0; r < C::BROWS; ++r) {
-      const int nr = brow0 + C::RPPB * r;
-      const bool ok = nr < BN && n0 + nr < d.N;
-      const int n = ok ? n0 + nr : 0;
-      st.b[r] = *reinterpret_cast<const u32x4*>(bsrc + (size_t)n * d.Kp + kt * BK + bq * 8);
-      if (ok) st.bok |= 1u << r;
-    }
+    for (int r = 0; r < C::BROWS; ++r) st.b[r] = __builtin_amdgcn_raw_buffer_load_b128(brs, (int)boff[r], koff, 0);
   };
 
   auto store_tile = [&](int buf, const Set& st) {
     _Float16* ahi = hl + buf * C::STAGE;
     _Float16* alo = ahi + C::PA;
-    _Float16* bpl = ahi + 2 * C::PA + (cb >> 2) * C::PB;
+    _Float16* bpl = ahi + 2 * C::PA + plane * C::PB;
 #pragma unroll
     for (int r = 0; r < AROWS; ++r) {
       const f32x4 v = al.value(st.a, r);
@@ -271,8 +275,7 @@ conv_gemm_x3_kernel(const ConvDesc d) {
 #pragma unroll
     for (int r = 0; r < C::BROWS; ++r) {
       const int nr = brow0 + C::RPPB * r;
-      if (nr < BN)
-        *reinterpret_cast<u32x4*>(bpl + nr * C::LROW + bq * 8) = ((st.bok >> r) & 1) ? st.b[r] : u32x4{0u, 0u, 0u, 0u};
+      if (nr < BN) *reinterpret_cast<u32x4*>(bpl + nr * C::LROW + bq * 8) = st.b[r];
     }
   };
 
@@ -315,18 +318,21 @@ conv_gemm_x3_kernel(const ConvDesc d) {
   };
   if (kt0 < kt1) {
     load_tile(kt0, set0);
-    if (kt0 + 1 < kt1) load_tile(kt0 + 1, set1);
+    load_tile(min(kt0 + 1, kt1 - 1), set1);
     store_tile(0, set0);
     __syncthreads();
+    // The prefetches are unconditional (past the last K-tile they re-read it): a load that
+    // only some paths issue makes the compiler's wait counting assume the short path and
+    // wait for ALL loads (vmcnt(0)) before the LDS store, i.e. for the tile just issued.
     for (int kt = kt0; kt < kt1; kt += 2) {
       // even step: LDS buffer 0 holds kt, set 1 holds kt+1 (in flight), set 0 is free
-      if (kt + 2 < kt1) load_tile(kt + 2, set0);
+      load_tile(min(kt + 2, kt1 - 1), set0);
       compute(0);
       if (kt + 1 < kt1) store_tile(1, set1);
       __syncthreads();
       if (kt + 1 >= kt1) break;
       // odd step: buffer 1 holds kt+1, set 0 holds kt+2 (in flight), set 1 is free
-      if (kt + 3 < kt1) load_tile(kt + 3, set1);
+      load_tile(min(kt + 3, kt1 - 1), set1);
       compute(1);
       if (kt + 2 < kt1) store_tile(0, set0);
       __syncthreads();
@@ -403,10 +409,18 @@ hipError_t launch_cfg(const ConvDesc& d, hipStream_t s) {
   const bool s1 = d.s1.p != nullptr, add = d.s0.p2 != nullptr, pre = d.s0.pre_scale != nullptr;
   if ((int)s1 + (int)add + (int)pre > 1) return hipErrorInvalidValue;
   if (use_x3() && d.wh && d.wl) {
-    if (s1) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, true, false, false>), grid, block, 0, s, d);
-    else if (add) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, true, false>), grid, block, 0, s, d);
-    else if (pre) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, false, true>), grid, block, 0, s, d);
-    else hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, false, false>), grid, block, 0, s, d);
+    if (conv_buf_loader_ok(d, BM)) {
+      if (s1) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, true, false, false, true>), grid, block, 0, s, d);
+      else if (add) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, true, false, true>), grid, block, 0, s, d);
+      else if (pre) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, false, true, true>), grid, block, 0, s, d);
+      else hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, false, false, true>), grid, block, 0, s, d);
+    } else if (s1 || pre) {
+      return hipErrorInvalidValue;   // no generic-loader instantiation (conv_buf_loader_ok)
+    } else if (add) {
+      hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, true, false, false>), grid, block, 0, s, d);
+    } else {
+      hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, false, false, false>), grid, block, 0, s, d);
+    }
   } else if (s1) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, true, false, false>), grid, block, 0, s, d);
   else if (add) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, false, true, false>), grid, block, 0, s, d);
   else if (pre) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, false, false, true>), grid, block, 0, s, d);
@@ -441,7 +455,8 @@ std::string conv_kernel_name(const ConvDesc& d) {
   const std::string tail = std::to_string(c.wm) + ", " + std::to_string(c.wn) + ", " + (s1 ? "true" : "false") + ", " +
                            (add ? "true" : "false") + ", " + (pre ? "true" : "false") + ">";
   if (use_x3() && d.wh && d.wl)
-    return "conv_gemm_x3_kernel<" + std::to_string(c.bm) + ", " + std::to_string(c.bn) + ", " + tail;
+    return "conv_gemm_x3_kernel<" + std::to_string(c.bm) + ", " + std::to_string(c.bn) + ", " +
+           tail.substr(0, tail.size() - 1) + (conv_buf_loader_ok(d, c.bm) ? ", true>" : ", false>");
   return "conv_gemm_kernel<" + std::to_string(c.bm) + ", " + std::to_string(c.bn) + ", " + std::to_string(c.bk) + ", " +
          tail;
 }
