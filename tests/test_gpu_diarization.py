@@ -51,6 +51,11 @@ def test_diarization_matches_oracle(tmp_path):
     lab = cc.merge_by_cos(cc.filter_minor_cluster(lab, emb_ref, 0), emb_ref, 0.3)
     ref = diar_ref.compressed_seg([[c[0], c[1], int(j)] for c, j in zip(chunks, lab)])
     assert out == ref
+    # hence the same DER as the oracle pipeline, scored like the reference recipe (md-eval)
+    from speakerlab.utils import der
+    gt = [f'SPEAKER m 0 {a:.3f} {b - a:.3f} <NA> <NA> s{k} <NA> <NA>' for a, b, k in turns]
+    to_rttm = lambda segs: [f'SPEAKER m 0 {a:.3f} {b - a:.3f} <NA> <NA> {k} <NA> <NA>' for a, b, k in segs]
+    assert der.der(gt, to_rttm(out)) == der.der(gt, to_rttm(ref))
 
     rttm = tmp_path / 'm.rttm'
     diar.save_diar_output(str(rttm), 'm')

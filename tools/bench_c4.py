@@ -1,0 +1,153 @@
+"""Config C4 (BASELINE.json configs[3]): ERes2Net-large (22.46 M) over a 100k-utterance
+corpus of 2 s segments sharded across the GPUs of one node, ONE all-gather of the
+embeddings (RCCL over xGMI), then every rank scores its row block of the N x N cosine
+affinity (spk_cosine_affinity, MFMA) and consumes it on the spot: the best-matching other
+utterance of every row (top-1 trial score + index), so the 40 GB matrix never exists.
+
+    python tools/bench_c4.py [--utts 100000]                       # 1 GPU
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P tools/bench_c4.py                          # N GPUs (weak in GPUs, fixed corpus)
+
+Inputs: a pool of P distinct synthetic 2 s utterances (numpy PCG64, seed 1000 + i,
+SURVEY §8(d)); utterance u is pool[u % P] circularly shifted by 37 * (u // P) samples, so
+all 100k inputs differ.  Every rank builds its contiguous shard in HBM before the timed
+region (12.8 GB at N=1).  Timed region (barrier + synchronize on both sides, max over
+ranks): GPU Fbank + forward of the shard, the all-gather, the scoring pass.  Rank 0 prints
+one JSON line; stage times are HIP-event times on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (REPO, os.path.join(REPO, '3d-speaker_amd'), os.path.join(REPO, 'tests')):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+SAMPLES = 32000
+SHIFT = 37
+
+
+def build_shard(pool, start, stop, device):
+    P = pool.shape[0]
+    out = torch.empty((stop - start, SAMPLES), dtype=torch.float32, device=device)
+    ar = torch.arange(SAMPLES, device=device)
+    for a in range(start, stop, 4096):
+        b = min(stop, a + 4096)
+        u = torch.arange(a, b, device=device)
+        idx = (ar[None, :] - (u[:, None] // P) * SHIFT) % SAMPLES
+        out[a - start:b - start] = torch.gather(pool[u % P], 1, idx)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--utts', type=int, default=100_000)
+    ap.add_argument('--batch', type=int, default=256)
+    ap.add_argument('--pool', type=int, default=1024)
+    ap.add_argument('--chunk-rows', type=int, default=4096)
+    ap.add_argument('--warmup', type=int, default=2)
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    device = torch.device('cuda', local)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=device)
+
+    from speakerlab import _hip
+    from speakerlab.utils import synthetic
+    from speakerlab.utils.distributed import all_gather_embeddings, shard_bounds
+    import helpers
+
+    model = helpers.loaded_module('eres2net_large').to(device).eval()
+    E = 192
+    pool = torch.from_numpy(np.stack([synthetic.synth_wav(SAMPLES, 1000 + i) for i in range(args.pool)])).to(device)
+    s0, s1 = shard_bounds(args.utts, rank, world)
+    wav = build_shard(pool, s0, s1, device)
+    n_local = s1 - s0
+    emb_local = torch.empty((n_local, E), dtype=torch.float32, device=device)
+
+    def embed():
+        with torch.no_grad():
+            for a in range(0, n_local, args.batch):
+                b = min(n_local, a + args.batch)
+                feats = _hip.fbank(wav[a:b], 80, mean_nor=True)
+                emb_local[a:b] = model(feats)
+
+    def score(emb_all):
+        # top-1 trial score of every row of this rank's block against all N (self excluded)
+        best = torch.empty(n_local, dtype=torch.float32, device=device)
+        arg = torch.empty(n_local, dtype=torch.int64, device=device)
+        chunk = torch.empty((args.chunk_rows, emb_all.shape[0]), dtype=torch.float32, device=device)
+        for a in range(0, n_local, args.chunk_rows):
+            b = min(n_local, a + args.chunk_rows)
+            c = chunk[:b - a]
+            _hip.cosine_affinity(emb_all[s0 + a:s0 + b], emb_all, out=c)
+            r = torch.arange(b - a, device=device)
+            c[r, s0 + a + r] = -2.0
+            best[a:b], arg[a:b] = c.max(dim=1)
+        return best, arg
+
+    def gather():
+        if world > 1:
+            return all_gather_embeddings(emb_local, args.utts)
+        return emb_local
+
+    # warm-up: a few batches + one scoring chunk (kernels, workspaces, RCCL communicators)
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            model(_hip.fbank(wav[:args.batch], 80, mean_nor=True))
+        if world > 1:
+            all_gather_embeddings(emb_local[:min(n_local, 8)], min(args.utts, 8 * world))
+        _hip.cosine_affinity(emb_local[:256], emb_local[:1024])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    t0 = time.perf_counter()
+    ev[0].record()
+    embed()
+    ev[1].record()
+    emb_all = gather()
+    ev[2].record()
+    best, arg = score(emb_all)
+    ev[3].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    assert torch.isfinite(best).all() and emb_all.shape == (args.utts, E)
+    if rank == 0:
+        ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(3)]
+        flop_embed = model._hip_handle(device).flops(198) * args.utts
+        flop_score = 2.0 * E * args.utts * args.utts
+        print(json.dumps({
+            'metric': 'utterance-embeddings/sec (2 s @16 kHz), ERes2Net-large shard + all-gather + cosine scoring',
+            'workload': 'c4', 'value': round(args.utts / dt, 1), 'unit': 'utt/s', 'n_gpus': world,
+            'utterances': args.utts, 'seconds': round(dt, 3), 'scaling': 'strong (fixed corpus)',
+            'stage_ms_rank0': {'embed': round(ms[0], 1), 'all_gather': round(ms[1], 2), 'score_top1': round(ms[2], 1)},
+            'embed_tflops_per_gpu': round(flop_embed / world / (ms[0] * 1e-3) / 1e12, 1),
+            'score_tflops_per_gpu': round(flop_score / world / (ms[2] * 1e-3) / 1e12, 1),
+            'top1_mean_score': round(float(best.mean()), 4),
+            'dtype': 'f32 (fp16x3 MFMA convs, fp32 MFMA affinity)',
+            'data': f'synthetic: {args.pool} PCG64 utterances (seed 1000+i), circular shifts make {args.utts} distinct inputs',
+            'parallelism': f'dp{world}: contiguous shards, 1 all-gather (RCCL), row-block scoring'}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

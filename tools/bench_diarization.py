@@ -31,7 +31,7 @@ def main():
     args = ap.parse_args()
     from speakerlab.bin import infer_diarization as idz
     from speakerlab.process import cluster
-    from speakerlab.utils import synthetic, vad_post
+    from speakerlab.utils import der, synthetic, vad_post
 
     t = {}
     t0 = time.perf_counter()
@@ -56,12 +56,21 @@ def main():
     t['embeddings_s'] = time.perf_counter() - t0
     res = {'workload': 'c5', 'audio_s': round(len(wav) / 16000, 1), 'speakers': args.speakers,
            'vad_segments': len(vad_time), 'chunks': len(chunks), 'embed_batch': args.batch}
+    # DER against the generator's ground-truth turns, scored like the reference recipe
+    # (egs/.../local/DER.py + md-eval.pl: collar 0, overlap scored; speakerlab/utils/der.py)
+    ref_rttm = [f'SPEAKER meeting 0 {st:.3f} {ed - st:.3f} <NA> <NA> spk{k} <NA> <NA>' for st, ed, k in turns]
+
+    def der_of(segs):
+        sys_rttm = [f'SPEAKER meeting 0 {st:.3f} {ed - st:.3f} <NA> <NA> {k:d} <NA> <NA>' for st, ed, k in segs]
+        return {k: round(v, 3) for k, v in der.der(ref_rttm, sys_rttm).items() if k != 'scored_speaker_time'}
+
     if args.cluster in ('ahc', 'both'):
         t0 = time.perf_counter()
         _, segs = diar.do_clustering(chunks, emb)
         t['cluster_ahc_s'] = time.perf_counter() - t0
         res['ahc_speakers'] = len({s[2] for s in segs})
         res['ahc_segments'] = len(segs)
+        res['ahc_der'] = der_of(segs)
     if args.cluster in ('spectral', 'both'):
         cc = cluster.CommonClustering('spectral', mer_cos=0.8, min_cluster_size=4)
         np.random.seed(0)
@@ -86,6 +95,11 @@ def main():
         _hip.symmetric_eig(L)
         res['syevd_s'] = round(time.perf_counter() - t0, 4)
         res['spectral_speakers'] = int(len(np.unique(labels)))
+        res['spectral_der'] = der_of(vad_post.compressed_seg([[c[0], c[1], int(j)] for c, j in zip(chunks, labels)]))
+        # the same back-end told the true speaker count (the CLI's --speaker_num)
+        np.random.seed(0)
+        lk = cc(emb, speaker_num=args.speakers)
+        res['spectral_k_der'] = der_of(vad_post.compressed_seg([[c[0], c[1], int(j)] for c, j in zip(chunks, lk)]))
     total = sum(v for k, v in t.items() if k != 'synth_s')
     res.update({k: round(v, 3) for k, v in t.items()})
     res['pipeline_s'] = round(total, 3)
