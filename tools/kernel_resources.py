@@ -2,6 +2,7 @@
 
 Usage: python tools/kernel_resources.py 3d-speaker_amd/csrc/conv_gemm.hip [more.hip ...]
 """
+import os
 import re
 import subprocess
 import sys
@@ -11,7 +12,7 @@ CSRC = '3d-speaker_amd/csrc'
 
 def main():
     for src in sys.argv[1:]:
-        p = subprocess.run(['hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-I', CSRC, '-c', src,
+        p = subprocess.run(['hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-I', CSRC, '-c', src] + os.environ.get('KR_FLAGS', '').split() + [
                             '-o', '/dev/null', '-Rpass-analysis=kernel-resource-usage'],
                            capture_output=True, text=True)
         cur = None
