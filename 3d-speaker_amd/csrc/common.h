@@ -64,6 +64,14 @@ struct ConvDesc {
   const int* rowlen = nullptr;  // ragged batches: outputs with wo >= rowlen[img] are written as 0
 };
 
+// XCD-aware bijective block remap: consecutive logical ids (same M tile, all N tiles) are
+// placed on one XCD so the A tile they share stays in that XCD's L2 (the dispatcher deals
+// blocks round-robin over the 8 XCDs; cdna_hip_programming.md §5.5 T1, bijective form).
+__device__ __forceinline__ int xcd_remap(int orig, int nblk) {
+  const int q = nblk / 8, r = nblk % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
 // true when output row m is past its image's valid length (ragged batches)
 __host__ __device__ inline bool row_masked(const ConvDesc& d, int m) {
   if (!d.rowlen) return false;

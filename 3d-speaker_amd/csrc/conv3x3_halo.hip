@@ -21,6 +21,7 @@
 
 #include "common.h"
 #include "conv_epilogue.h"
+#include "conv_loader.h"
 
 #ifndef SPK_EXP
 #define SPK_EXP 0
@@ -334,23 +335,36 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
   const int tstride = gridDim.x / nsplit;
   const int n0 = slice * C::NP;
 
+  // Halo element r of this thread: quad qq (the same for every r, NT % QP == 0) of halo
+  // pixel p = tid / QP + (NT / QP) * r.  Its (row, column) in the halo is tile-invariant,
+  // so it is computed once and kept packed (row << 16 | column); elements past the halo and
+  // padding quads get a row no image has.  Per tile a load then costs an add, two unsigned
+  // bounds compares and one buffer load through a per-image resource (out-of-range offsets
+  // read zeros), instead of a divide chain and 64-bit address arithmetic.
+  static_assert(C::NT % C::QP == 0, "halo quads must tile the block");
+  const int qq = tid % C::QP;
+  uint32_t hrc[C::PF];
+#pragma unroll
+  for (int r = 0; r < C::PF; ++r) {
+    const int idx = tid + C::NT * r;
+    const int p = idx / C::QP;
+    hrc[r] = (idx < hq && qq < C::Q) ? ((uint32_t)(p / HW) << 16) | (uint32_t)(p % HW) : 0x7FFF0000u;
+  }
+  const size_t img_px = (size_t)H * W;
   f32x4 pa[C::PF], pb[ADD ? C::PF : 1];
-  unsigned pok = 0;
   auto pf_load = [&](int t) {
     const int img = t / (ntx * nty), ty = (t / ntx) % nty, tx = t % ntx;
     const int y0 = ty * TH - 1, x0 = tx * TW - 1;
-    pok = 0;
+    const __amdgpu_buffer_rsrc_t r0 = make_rsrc(d.s0.p + img * img_px * d.s0.ld);
+    __amdgpu_buffer_rsrc_t r2;
+    if (ADD) r2 = make_rsrc(d.s0.p2 + img * img_px * d.s0.ld2);
 #pragma unroll
     for (int r = 0; r < C::PF; ++r) {
-      const int idx = tid + C::NT * r;
-      const int q = idx % C::QP, p = idx / C::QP;
-      const int gy = y0 + p / HW, gx = x0 + p % HW;
-      const bool ok = idx < hq && q < C::Q && gy >= 0 && gy < H && gx >= 0 && gx < W;
-      const size_t pix = ok ? (size_t)(img * H + gy) * W + gx : 0;
-      const int c = ok ? 4 * q : 0;
-      pa[r] = *reinterpret_cast<const f32x4*>(d.s0.p + pix * d.s0.ld + c);
-      if (ADD) pb[r] = *reinterpret_cast<const f32x4*>(d.s0.p2 + pix * d.s0.ld2 + c);
-      pok |= ok ? 1u << r : 0u;
+      const int gy = y0 + (int)(hrc[r] >> 16), gx = x0 + (int)(hrc[r] & 0xFFFFu);
+      const bool ok = (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+      const uint32_t pix = (uint32_t)(gy * W + gx);
+      pa[r] = buf_load4(r0, ok ? (pix * (uint32_t)d.s0.ld + 4u * qq) * 4u : BUF_OOB);
+      if (ADD) pb[r] = buf_load4(r2, ok ? (pix * (uint32_t)d.s0.ld2 + 4u * qq) * 4u : BUF_OOB);
     }
   };
   auto pf_store = [&]() {
@@ -360,8 +374,7 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
       if (idx < hq) {
         f32x4 v = pa[r];
         if (ADD) v += pb[r];
-        if (!((pok >> r) & 1)) v = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int q = idx % C::QP, p = idx / C::QP;
+        const int q = qq, p = idx / C::QP;
         f16x4 h, l;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -577,7 +590,9 @@ bool halo_conv_supported(const ConvDesc& d) {
   return s.kh == 3 && s.kw == 3 && s.sh == 1 && s.sw == 1 && s.ph == 1 && s.pw == 1 && s.dh == 1 && s.dw == 1 &&
          !s.reflect && !s.pre_scale && !d.s1.p && d.s1.cin == 0 && d.ksplit == 1 && d.N <= 64 &&
          (s.cin == 28 || s.cin == 32 || s.cin == 52 || s.cin == 64) && d.Ho == s.H && d.Wo == s.W &&
-         d.Kp >= 9 * s.cin && s.ld % 4 == 0 && (!s.p2 || s.ld2 % 4 == 0);
+         d.Kp >= 9 * s.cin && s.ld % 4 == 0 && (!s.p2 || s.ld2 % 4 == 0) &&
+         // the x3 kernel addresses one image through a buffer resource (32-bit offsets)
+         (double)s.H * s.W * std::max(s.ld, s.p2 ? s.ld2 : 0) * 4.0 < 0x7FFFFFF0 - 64;
 }
 
 std::string halo_kernel_name(const ConvDesc& d) {

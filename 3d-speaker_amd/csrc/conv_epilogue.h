@@ -124,6 +124,51 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
       }
       return;
     }
+    // AFF second conv (fusion.py:26-28): x*(1+tanh v) + y*(1-tanh v) replaces the
+    // activations; both operands of every row of the wave are in flight before first use.
+    if (!LEAN && vec && !part && d.affx && !d.res && !d.gate && !d.rowbias) {
+      const int c4 = (lane & 7) * 4;
+      f32x4 xa[NTL][4], ya[NTL][4];
+#pragma unroll
+      for (int tile = 0; tile < NTL; ++tile) {
+        const int i = tile / TN, j = tile % TN;
+        const int n = nwave + j * 32 + c4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          xa[tile][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+          ya[tile][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (n < d.N) {
+            const int m = max(0, min(rowmap(i * 32 + q * 8 + (lane >> 3)), M - 1));
+            xa[tile][q] = *reinterpret_cast<const f32x4*>(d.affx + (size_t)m * d.ldx + n);
+            ya[tile][q] = *reinterpret_cast<const f32x4*>(d.affy + (size_t)m * d.ldy + n);
+          }
+        }
+      }
+#pragma unroll
+      for (int tile = 0; tile < NTL; ++tile) {
+        const int i = tile / TN, j = tile % TN;
+        const int n = nwave + j * 32 + c4;
+        if (n >= d.N) continue;
+        f32x4 bias = {0.f, 0.f, 0.f, 0.f};
+        if (d.bias) bias = *reinterpret_cast<const f32x4*>(d.bias + n);
+        const float* ct = cw + tile * 1024;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rl = q * 8 + (lane >> 3);
+          const int m = rowmap(i * 32 + rl);
+          if (m < 0 || m >= M) continue;
+          f32x4 o = *reinterpret_cast<const f32x4*>(ct + rl * 32 + c4) + bias;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float t = 1.0f + tanhf(o[e]);
+            o[e] = xa[tile][q][e] * t + ya[tile][q][e] * (2.0f - t);
+          }
+          if (row_masked(d, m)) o = f32x4{0.f, 0.f, 0.f, 0.f};
+          *reinterpret_cast<f32x4*>(d.out + (size_t)m * d.ldo + n) = o;
+        }
+      }
+      return;
+    }
   }
   if constexpr (LEAN) return;
 #pragma unroll 1

@@ -30,14 +30,6 @@ namespace {
 
 constexpr int KP_ALIGN = 32;   // weights are packed with Kp a multiple of this
 
-// XCD-aware bijective block remap: consecutive logical ids (same M tile, all N tiles) are
-// placed on one XCD so the A tile they share stays in that XCD's L2
-// (cdna_hip_programming.md §5.5 T1, bijective form).
-__device__ __forceinline__ int xcd_remap(int orig, int nblk) {
-  const int q = nblk / 8, r = nblk % 8, xcd = orig % 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
-}
-
 template <int BM, int BN, int BK, int WM, int WN, bool S1, bool ADD, bool PRE>
 __global__ void __launch_bounds__(64 * WM * WN, 4)
 conv_gemm_kernel(const ConvDesc d) {

@@ -59,12 +59,17 @@ struct ERes2Builder {
 
   double pix(const T4& t) const { return (double)t.H * t.W; }
 
+  // AFF bottleneck layout: C/4 channels, padded to at least 32 so the second 1x1 conv's
+  // K-tile is one whole tap and the buffer-resource loader applies (conv_buf_loader_ok);
+  // the padding channels have zero weights and bias, so they hold silu(0) = 0.
+  static ChanMap aff_mid(int C) { return ChanMap::dense(C / 4, C / 4 < 32 ? 32 : 4); }
+
   // AFF(x, y) -> out (fusion.py:22-28); x, y, out share geometry, C logical channels each.
   void aff(const std::string& p, const T4& x, const T4& y, int C, const T4& out) {
     const int inter = C / 4;
     const ChanMap xin = ChanMap::dense(C);
     const int cp = xin.n_phys;
-    const ChanMap mid = ChanMap::dense(inter);
+    const ChanMap mid = aff_mid(C);
     const Packed& a0 = m.pack(p + ".la0", mid,
                               {Part{p + ".local_att.0.weight", p + ".local_att.0.bias", p + ".local_att.1", xin, 0, 0},
                                Part{p + ".local_att.0.weight", p + ".local_att.0.bias", p + ".local_att.1", xin, C, cp}},
@@ -213,7 +218,7 @@ struct ERes2Builder {
         mid_max = std::max(mid_max, px * ChanMap::dense(width / 4).n_phys);
         fb_max = std::max(fb_max, px * ChanMap::dense(width).n_phys);
         const int C = (mc << li) * expansion;   // model-level AFF at this resolution
-        mid_max = std::max(mid_max, px * ChanMap::dense(C / 4).n_phys);
+        mid_max = std::max(mid_max, px * aff_mid(C).n_phys);
       }
     }
     T1 = b.alloc(t1_max);

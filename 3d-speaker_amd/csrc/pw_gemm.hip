@@ -55,11 +55,14 @@ pw_gemm_x3_kernel(const ConvDesc d) {
   const int wm = wave / C::WN, wn = wave % C::WN;
   const int M = d.nimg * d.Ho * d.Wo;
   const int nN = (d.N + BN - 1) / BN;
-  const int nb = blockIdx.x % nN;                          // this block's N-slice (fixed)
+  // the nN blocks of one M-tile walk get neighbouring logical ids, i.e. one XCD: the A
+  // tiles they all read come from one L2
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int nb = bid % nN;                                 // this block's N-slice (fixed)
   const int n0 = nb * BN;
   const int mtiles = (M + C::BM - 1) / C::BM;
   const int mstride = gridDim.x / nN;
-  const int mt0 = blockIdx.x / nN;
+  const int mt0 = bid / nN;
   const int K0 = d.s0.cin;                                 // s0 channels, then s1 (S1)
   const int K = d.K;
 
