@@ -147,11 +147,12 @@ Buf Builder::alloc(size_t floats) {
   return b;
 }
 
-void Builder::step(const std::string& name, Step s, const std::string& kernel) {
+void Builder::step(const std::string& name, Step s, const std::string& kernel, double bytes) {
   if (!plan) return;
   plan->steps.push_back(std::move(s));
   plan->names.push_back(name);
   plan->kernels.push_back(kernel.empty() ? name : kernel);
+  plan->bytes.push_back(bytes);
   plan->flops.push_back(2.0 * (macs_per_utt - macs_at_last_step) * B);
   macs_at_last_step = macs_per_utt;
 }
@@ -180,6 +181,16 @@ void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const C
   static const int kDummyLen = 0;   // naming probe only: marks the ragged masks as present
   probe.rowlen = io.rowlen ? &kDummyLen : nullptr;
   probe.s0.vlen = io.vlen ? &kDummyLen : nullptr;
+  // algorithmic HBM bytes (SURVEY §8(d) pricing: every operand once, fp32): the input
+  // pixels the conv reads (all of them for a k > 1 window, the strided subset for a 1x1),
+  // the Res2Net addend, the K-concatenated second operand, weights, output, residual and
+  // the two AFF operands
+  const double px_out = (double)M;
+  const double a_px = (d.s0.kh == 1 && d.s0.kw == 1) ? px_out : (double)d.nimg * d.s0.H * d.s0.W;
+  double bytes = 4.0 * a_px * d.s0.cin * (io.s0b ? 2.0 : 1.0) + 4.0 * (double)d.N * d.K + 4.0 * px_out * d.N;
+  if (io.s1) bytes += 4.0 * px_out * d.s1.cin;
+  if (io.res) bytes += 4.0 * px_out * d.N;
+  if (io.affx) bytes += 8.0 * px_out * d.N;
   step(name, [d, cio](const Ctx& c) mutable {
     d.s0.p = c.resolve(cio.s0);
     d.s0.p2 = c.resolve(cio.s0b);
@@ -194,7 +205,7 @@ void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const C
     d.rowlen = c.resolve_i(cio.rowlen);
     d.s0.vlen = c.resolve_i(cio.vlen);
     return launch_conv(d, c.stream);
-  }, conv_kernel_name(probe));
+  }, conv_kernel_name(probe), bytes);
 }
 
 }  // namespace spk
@@ -570,6 +581,16 @@ int spk_model_plan_step(spk_model_t* model, int32_t B, int32_t T, int32_t i, cha
       kernel[kernel_len - 1] = 0;
     }
     if (flops) *flops = p->flops[i];
+    return SPK_OK;
+  });
+}
+
+int spk_model_plan_step_bytes(spk_model_t* model, int32_t B, int32_t T, int32_t i, double* bytes) {
+  return guarded([&]() -> int {
+    if (!model || !bytes || B <= 0 || T <= 0) return SPK_E_INVALID;
+    Plan* p = get_plan(model, B, T);
+    if (i < 0 || i >= (int)p->steps.size()) return SPK_E_INVALID;
+    *bytes = p->bytes[i];
     return SPK_OK;
   });
 }

@@ -55,6 +55,7 @@ struct Plan {
   std::vector<std::string> names;   // for error messages / tracing
   std::vector<std::string> kernels; // kernel instantiation each step launches
   std::vector<double> flops;        // algorithmic FLOPs of the step (whole batch)
+  std::vector<double> bytes;        // algorithmic HBM bytes of the step (each operand once; 0 = not priced)
   size_t ws_bytes = 0;
   // hipGraph replay: the plan's launches captured once per workspace address, reading the
   // input / lengths from and writing the output to staging regions of the workspace
@@ -134,7 +135,7 @@ struct Builder {
   bool ragged = false;       // per-utterance lengths (Buf::LEN) mask the time axis
   Builder(Model& mm, Plan* p, int b, bool rg = false) : m(mm), plan(p), B(b), ragged(rg) {}
   Buf alloc(size_t floats);
-  void step(const std::string& name, Step s, const std::string& kernel = "");
+  void step(const std::string& name, Step s, const std::string& kernel = "", double bytes = 0.0);
   // emit an implicit-GEMM conv; pointers of `d` are taken from the Bufs
   struct ConvIO {
     Buf s0, s0b, s1, out, res, affx, affy, gate, partial, rowbias;

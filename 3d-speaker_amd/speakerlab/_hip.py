@@ -58,6 +58,8 @@ SYMBOLS = {
     'spk_model_plan_step': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p,
                                            ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32,
                                            ctypes.POINTER(ctypes.c_double)]),
+    'spk_model_plan_step_bytes': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                 ctypes.POINTER(ctypes.c_double)]),
     'spk_model_forward_timed': (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_size_t, _P, _P,
                                                _P, ctypes.c_int32]),
     'spk_cosine_affinity': (ctypes.c_int, [_P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int32, _P,
@@ -242,6 +244,15 @@ class NativeModel:
             _check(lib().spk_model_plan_step(self.handle, B, T, i, name, 256, kern, 256, ctypes.byref(fl)),
                    'spk_model_plan_step')
             out.append((name.value.decode(), kern.value.decode(), fl.value))
+        return out
+
+    def plan_bytes(self, B: int, T: int):
+        """Algorithmic HBM bytes of every plan step (0 where a step is not priced)."""
+        out = []
+        for i in range(len(self.plan(B, T))):
+            b = ctypes.c_double()
+            _check(lib().spk_model_plan_step_bytes(self.handle, B, T, i, ctypes.byref(b)), 'spk_model_plan_step_bytes')
+            out.append(b.value)
         return out
 
     def forward_timed(self, feats: torch.Tensor, out: torch.Tensor):

@@ -73,15 +73,33 @@ def roofline(model, feats, device, traffic_json):
     times = None
     for _ in range(3):                        # keep the last of 3 (warm)
         times = h.forward_timed(feats, out)
+    nbytes = h.plan_bytes(B, T)
     groups = {}
-    for (name, kern, fl), ms in zip(plan, times):
-        g = groups.setdefault(kern, {'ms': 0.0, 'flops': 0.0, 'launches': 0})
+    for (name, kern, fl), by, ms in zip(plan, nbytes, times):
+        g = groups.setdefault(kern, {'ms': 0.0, 'flops': 0.0, 'bytes': 0.0, 'launches': 0, 'steps': []})
         g['ms'] += ms
         g['flops'] += fl
+        g['bytes'] += by
         g['launches'] += 1
+        g['steps'].append((fl, by, ms))
     kern, g = max(groups.items(), key=lambda kv: kv[1]['ms'])
     x3 = '_x3_' in kern
     peak = PEAK_X3_TFLOPS if x3 else PEAK_FP32_TFLOPS
+
+    def attainable(steps, pk):
+        """Per-launch roofline: each launch needs at least max(FLOPs / MFMA peak, algorithmic
+        bytes / HBM peak); summed over launches and compared with the measured time."""
+        t_min = n_mfma = n_hbm = 0
+        for fl, by, _ in steps:
+            tf, tb = fl / (pk * 1e12), by / (PEAK_HBM_GBS * 1e9)
+            t_min += max(tf, tb)
+            n_mfma += tf >= tb
+            n_hbm += tb > tf
+        t = sum(ms for _, _, ms in steps) * 1e-3
+        return {'attainable_ms': round(t_min * 1e3, 3), 'measured_ms': round(t * 1e3, 3),
+                'frac': round(t_min / t, 4) if t else None,
+                'launches_mfma_bound': int(n_mfma), 'launches_hbm_bound': int(n_hbm),
+                'hbm_achieved_GBs': round(sum(by for _, by, _ in steps) / t / 1e9, 1) if t else None}
     avg_ms = g['ms'] / g['launches']
     flops_per_launch = g['flops'] / g['launches']
     achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
@@ -112,6 +130,12 @@ def roofline(model, feats, device, traffic_json):
         'all_conv_kernels': {'achieved': round(conv_fl / (conv_ms * 1e-3) / 1e12, 3),
                           'frac_of_x3_peak': round(conv_fl / (conv_ms * 1e-3) / 1e12 / PEAK_X3_TFLOPS, 4),
                           'ms_per_forward': round(conv_ms, 3)},
+        'per_launch_roofline': dict(
+            attainable(g['steps'], peak),
+            basis='sum over the launches of max(algorithmic FLOPs / MFMA peak, algorithmic bytes / '
+                  '8 TB/s) vs measured; bytes = every operand once (spk_model_plan_step_bytes)'),
+        'all_conv_per_launch_roofline': attainable(
+            [st for k, v in groups.items() if is_conv(k) for st in v['steps']], PEAK_X3_TFLOPS if x3 else peak),
         'forward_ms_sum_of_steps': round(sum(times), 3),
         'per_kernel_ms': {k: round(v['ms'], 3) for k, v in sorted(groups.items(), key=lambda kv: -kv[1]['ms'])},
     }

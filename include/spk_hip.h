@@ -123,6 +123,9 @@ int spk_model_flops(spk_model_t* model, int32_t T, double* flops);
 int spk_model_plan_size(spk_model_t* model, int32_t B, int32_t T, int32_t* n_steps);
 int spk_model_plan_step(spk_model_t* model, int32_t B, int32_t T, int32_t i, char* name, int32_t name_len,
                         char* kernel, int32_t kernel_len, double* flops);
+/* Algorithmic HBM bytes of plan step i (every operand read / written once, fp32; conv
+ * steps only, 0 for steps that are not priced): the byte side of the per-launch roofline. */
+int spk_model_plan_step_bytes(spk_model_t* model, int32_t B, int32_t T, int32_t i, double* bytes);
 int spk_model_forward_timed(spk_model_t* model, const float* feats, int32_t B, int32_t T, void* workspace,
                             size_t workspace_bytes, float* emb_out, void* stream, float* step_ms,
                             int32_t max_steps);

@@ -85,6 +85,14 @@ class EmuModel:
             steps.append((name.value.decode(), fl.value, kern.value.decode()))
         return steps
 
+    def plan_bytes(self, B, T):
+        out = []
+        for i in range(len(self.plan(B, T))):
+            b = ctypes.c_double()
+            _check(lib().spk_model_plan_step_bytes(self.handle, B, T, i, ctypes.byref(b)), 'step_bytes')
+            out.append(b.value)
+        return out
+
     def flops(self, T):
         f = ctypes.c_double()
         _check(lib().spk_model_flops(self.handle, T, ctypes.byref(f)), 'flops')

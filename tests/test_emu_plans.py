@@ -72,3 +72,21 @@ def test_emulated_ragged_campplus_matches_per_utterance(arch):
     for b, n in enumerate(lengths):
         ref = models_ref.forward(arch, sd, full[b:b + 1, :n].double()).numpy()
         assert helpers.rel_err(emb[b:b + 1], ref).max() < 1e-5, (b, n)
+
+
+def test_step_bytes_priced_per_conv():
+    """Per-step algorithmic bytes (the byte side of bench.py's per-launch roofline): every
+    conv step is priced, and ERes2NetV2 layer1.1.conv3 (1x1, 56 -> 128 channels, residual)
+    is exactly input + weights + output + residual, fp32."""
+    m = helpers.loaded_module('eres2netv2')
+    em = EmuModel(m)
+    B, T = 2, 40
+    steps = em.plan(B, T)
+    nbytes = em.plan_bytes(B, T)
+    assert len(nbytes) == len(steps)
+    for (name, _, kern), by in zip(steps, nbytes):
+        if kern.startswith(('conv_gemm', 'conv3x3', 'pw_gemm')):
+            assert by > 0, name
+    i = [name for name, _, _ in steps].index('layer1.1.conv3')
+    px = B * 80 * T
+    assert nbytes[i] == 4.0 * (px * 56 + 128 * 56 + px * 128 + px * 128)
