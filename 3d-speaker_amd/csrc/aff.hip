@@ -1,0 +1,207 @@
+// Fused AFF (fusion.py:8-28) on fp16x3 MFMA, gfx950:
+//   h   = SiLU(BN(W1 · cat(x, y) + b1))          (local_att.0-2, K = 2C, N = C/4)
+//   z   = BN(W2 · h + b2)                        (local_att.3-4, K = C/4, N = C)
+//   out = x · (1 + tanh z) + y · (1 − tanh z)
+// The two-conv form moves x and y through HBM twice and the bottleneck h once each way;
+// here one wave owns 32 pixels end to end and nothing but x, y (once) and out touch HBM.
+//
+// Both GEMMs are computed transposed (pixels along the MFMA columns), so that stage 1's
+// accumulator layout (lane = pixel, registers = bottleneck channels) is exactly the B
+// operand layout stage 2 needs: no LDS round trip between the stages.
+//   stage 1: hT[j][m] = sum_k W1[j][k] · xy[m][k]   A = W1 (rows j), B = xy^T (columns m)
+//   stage 2: zT[n][m] = sum_j W2[n][j] · hT[j][m]   A = W2 (rows n), B = hT
+// 32x32x16 MFMA C layout: lane l holds column l&31, rows (r&3) + 8(r>>2) + 4(l>>5), r < 16.
+// For stage 2's k-step (t, s) lane half h therefore supplies bottleneck channels
+// 32t + 16s + 4h + {0..3} and 32t + 16s + 8 + 4h + {0..3}, and its W2 fragments are read in
+// the same order.  Stage 1 uses the k permutation of the conv GEMM (lane half h owns
+// k0 + 16h .. +15 of a 32-deep step, the two 16-deep MFMA steps take 8 each), so every lane
+// reads 64 contiguous bytes of its pixel's [x | y] row per step.
+// fp16x3 as in conv_gemm.hip: hi = fp16(v), lo = fp16((v − hi)·2^11), three products.
+#include <algorithm>
+#include <cstdlib>
+
+#include "aff.h"
+#include "conv_epilogue.h"
+
+namespace spk {
+
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split8(const f32x4 a, const f32x4 b, f16x8& hi, f16x8& lo) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const _Float16 ha = (_Float16)a[e], hb = (_Float16)b[e];
+    hi[e] = ha;
+    hi[e + 4] = hb;
+    lo[e] = (_Float16)((a[e] - (float)ha) * 2048.0f);
+    lo[e + 4] = (_Float16)((b[e] - (float)hb) * 2048.0f);
+  }
+}
+
+__device__ __forceinline__ f16x8 ld_h8(const uint16_t* p) { return *reinterpret_cast<const f16x8*>(p); }
+__device__ __forceinline__ f16x4 ld_h4(const uint16_t* p) { return *reinterpret_cast<const f16x4*>(p); }
+
+template <int MT>   // bottleneck tiles of 32 channels
+__global__ void __launch_bounds__(256) aff_x3_kernel(const AffDesc a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int m0 = (blockIdx.x * 4 + wave) * 32;
+  if (m0 >= a.M) return;                            // wave-uniform; no block barriers below
+  const bool mok = m0 + li < a.M;
+  const int m = mok ? m0 + li : a.M - 1;            // this lane's pixel
+  const float* xr = a.x + (size_t)m * a.ldx;
+  const float* yr = a.y + (size_t)m * a.ldy;
+  const int K = 2 * a.cp;
+
+  // ---- stage 1
+  f32x16 h[MT], hx[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { h[t][r] = 0.f; hx[t][r] = 0.f; }
+  // [x | y] loads run one 32-deep step ahead of the MFMAs (clamped in-row addresses,
+  // zeroed past K when used, so the prefetch is unconditional)
+  auto load_xy = [&](int k0, f32x4 (&v)[2][2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {                   // 8 channels each, from x or y (cp % 8 == 0)
+      const int k = min(k0 + 16 * lh + 8 * s, K - 8);
+      const float* src = k < a.cp ? xr + k : yr + (k - a.cp);
+      v[s][0] = *reinterpret_cast<const f32x4*>(src);
+      v[s][1] = *reinterpret_cast<const f32x4*>(src + 4);
+    }
+  };
+  f32x4 vn[2][2];
+  load_xy(0, vn);
+  for (int k0 = 0; k0 < K; k0 += 32) {
+    f32x4 v[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bool kin = k0 + 16 * lh + 8 * s < K;
+      v[s][0] = kin ? vn[s][0] : f32x4{0.f, 0.f, 0.f, 0.f};
+      v[s][1] = kin ? vn[s][1] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    load_xy(min(k0 + 32, K - 8), vn);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int k = k0 + 16 * lh + 8 * s;
+      f16x8 bh, bl;
+      split8(v[s][0], v[s][1], bh, bl);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        f16x8 ah = {}, al = {};
+        if (k < K) {                                // k + 7 < K <= kp1: inside the packed row
+          const size_t wo = (size_t)(t * 32 + li) * a.kp1 + k;
+          ah = ld_h8(a.w1h + wo);
+          al = ld_h8(a.w1l + wo);
+        }
+        h[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, h[t], 0, 0, 0);
+        hx[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, hx[t], 0, 0, 0);
+        hx[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, hx[t], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- bias + SiLU, split: stage 2's B fragments straight from the accumulators
+  f16x8 gh[MT][2], gl[MT][2];
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int j = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      float v = h[t][r] + hx[t][r] * (1.0f / 2048.0f) + a.b1[j];
+      v = v * __frcp_rn(1.0f + __expf(-v));         // SiLU
+      const _Float16 vh = (_Float16)v;
+      gh[t][r >> 3][r & 7] = vh;
+      gl[t][r >> 3][r & 7] = (_Float16)((v - (float)vh) * 2048.0f);
+    }
+
+  // ---- stage 2 + AFF combine, 32 output channels at a time
+  for (int n0 = 0; n0 < a.cp; n0 += 32) {
+    const int n = min(n0 + li, a.cp - 1);           // W2 row of this lane (A operand)
+    const bool nok = n0 + li < a.cp;
+    // lane: pixel m, channels n0 + 8q + 4h + {0..3} in registers 4q .. 4q+3; the combine's
+    // operands are requested before the MFMAs
+    f32x4 xv[4], yv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = min(n0 + 8 * q + 4 * lh, a.cp - 4);
+      xv[q] = *reinterpret_cast<const f32x4*>(xr + c);
+      yv[q] = *reinterpret_cast<const f32x4*>(yr + c);
+    }
+    f32x16 z, zx;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { z[r] = 0.f; zx[r] = 0.f; }
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const size_t wo = (size_t)n * a.kp2 + t * 32 + 16 * s + 4 * lh;
+        const f16x4 h0 = ld_h4(a.w2h + wo), h1 = ld_h4(a.w2h + wo + 8);
+        const f16x4 l0 = ld_h4(a.w2l + wo), l1 = ld_h4(a.w2l + wo + 8);
+        f16x8 ah = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        f16x8 al = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+        if (!nok) { ah = f16x8{}; al = f16x8{}; }
+        z = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gh[t][s], z, 0, 0, 0);
+        zx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gl[t][s], zx, 0, 0, 0);
+        zx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, gh[t][s], zx, 0, 0, 0);
+      }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = n0 + 8 * q + 4 * lh;
+      if (!mok || c >= a.cp) continue;
+      const f32x4 bias = *reinterpret_cast<const f32x4*>(a.b2 + c);
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        // x(1 + tanh z) + y(1 - tanh z) = 2(y + s(x - y)), s = sigmoid(2z): one exp + rcp
+        const float zz = z[4 * q + e] + zx[4 * q + e] * (1.0f / 2048.0f) + bias[e];
+        const float sg = __frcp_rn(1.0f + __expf(-2.0f * zz));
+        o[e] = 2.0f * fmaf(sg, xv[q][e] - yv[q][e], yv[q][e]);
+      }
+      *reinterpret_cast<f32x4*>(a.out + (size_t)m * a.ldo + c) = o;
+    }
+  }
+}
+
+}  // namespace
+
+bool aff_x3_supported(int cp, int nmid) {
+  static const bool off = [] {   // SPK_NO_AFF_FUSED=1: the two-conv form (experiments)
+    const char* e = std::getenv("SPK_NO_AFF_FUSED");
+    return e && std::atoi(e) != 0;
+  }();
+  // cp <= 208: past that (ERes2Net-large fuse_mode12, 256 channels at 40 x T/2) the rows of
+  // the pixels in flight no longer stay in L2 and the two-conv form is faster (measured)
+  return !off && conv_use_x3() && (nmid == 32 || nmid == 64) && cp % 8 == 0 && cp >= 8 && cp <= 208;
+}
+
+std::string aff_x3_kernel_name(int nmid) { return "aff_x3_kernel<" + std::to_string(nmid / 32) + ">"; }
+
+hipError_t launch_aff_x3(const AffDesc& a, hipStream_t s) {
+  // host-side shape checks: every vector access stays aligned and inside its row
+  if (!aff_x3_supported(a.cp, a.nmid) || a.M <= 0 || !a.w1h || !a.w1l || !a.w2h || !a.w2l || !a.b1 || !a.b2 ||
+      a.kp1 < 2 * a.cp || a.kp1 % 8 || a.kp2 < a.nmid || a.kp2 % 4 || a.ldx % 4 || a.ldy % 4 || a.ldo % 4 ||
+      a.ldx < a.cp || a.ldy < a.cp || a.ldo < a.cp ||
+      (reinterpret_cast<uintptr_t>(a.x) & 15) || (reinterpret_cast<uintptr_t>(a.y) & 15) ||
+      (reinterpret_cast<uintptr_t>(a.out) & 15) || (reinterpret_cast<uintptr_t>(a.w1h) & 15) ||
+      (reinterpret_cast<uintptr_t>(a.w1l) & 15))
+    return hipErrorInvalidValue;
+  const dim3 grid((a.M + 127) / 128), block(256);
+  // The combine re-reads the x / y rows stage 1 streamed; with every block slot filled the
+  // rows of the pixels in flight overflow the XCD's 4 MB L2 before they are re-read.  A
+  // 60 KB LDS reservation caps residency at 2 blocks (8 waves) per CU, which keeps them in
+  // L2 (measured: layer3 fusions 1.08 -> 0.97 ms per ERes2NetV2 forward; 1 block per CU
+  // is slower again).  SPK_AFF_LDS_KB overrides it for experiments.
+  static const size_t lds_pad = [] {
+    const char* e = std::getenv("SPK_AFF_LDS_KB");
+    return (size_t)(e ? std::atoi(e) : 60) * 1024;
+  }();
+  if (a.nmid == 32) hipLaunchKernelGGL(aff_x3_kernel<1>, grid, block, lds_pad, s, a);
+  else hipLaunchKernelGGL(aff_x3_kernel<2>, grid, block, lds_pad, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace spk

@@ -15,6 +15,7 @@
 //     applying x*(1+tanh a) + y*(1-tanh a) in its epilogue.
 #include <cmath>
 
+#include "aff.h"
 #include "misc.h"
 #include "runtime.h"
 
@@ -59,10 +60,11 @@ struct ERes2Builder {
 
   double pix(const T4& t) const { return (double)t.H * t.W; }
 
-  // AFF bottleneck layout: C/4 channels, padded to at least 32 so the second 1x1 conv's
-  // K-tile is one whole tap and the buffer-resource loader applies (conv_buf_loader_ok);
-  // the padding channels have zero weights and bias, so they hold silu(0) = 0.
-  static ChanMap aff_mid(int C) { return ChanMap::dense(C / 4, C / 4 < 32 ? 32 : 4); }
+  // AFF bottleneck layout: C/4 channels, up to 64 of them padded to a multiple of 32 (the
+  // fused kernel's MFMA tiles; for the two-conv form the second conv's K-tile is one whole
+  // tap, so the buffer-resource loader applies); padding channels have zero weights and
+  // bias, so they hold silu(0) = 0.
+  static ChanMap aff_mid(int C) { return ChanMap::dense(C / 4, C / 4 <= 64 ? 32 : 4); }
 
   // AFF(x, y) -> out (fusion.py:22-28); x, y, out share geometry, C logical channels each.
   void aff(const std::string& p, const T4& x, const T4& y, int C, const T4& out) {
@@ -80,6 +82,28 @@ struct ERes2Builder {
     const double m0 = pix(x) * 2.0 * C * inter, m3 = pix(x) * (double)inter * C;
     if (!b.plan) {
       b.macs_per_utt += m0 + m3;
+      return;
+    }
+    if (aff_x3_supported(cp, mid.n_phys)) {
+      // one fused kernel (aff.hip): x and y read once, h never leaves registers
+      b.macs_per_utt += m0 + m3;
+      AffDesc ad;
+      ad.M = b.B * x.H * x.W;
+      ad.cp = cp; ad.nmid = mid.n_phys;
+      ad.ldx = x.ld; ad.ldy = y.ld; ad.ldo = out.ld;
+      ad.w1 = m.dptr(a0.w_off); ad.w1h = m.dhi(a0.w_off); ad.w1l = m.dlo(a0.w_off);
+      ad.b1 = m.dptr(a0.b_off); ad.kp1 = a0.Kp;
+      ad.w2 = m.dptr(a1.w_off); ad.w2h = m.dhi(a1.w_off); ad.w2l = m.dlo(a1.w_off);
+      ad.b2 = m.dptr(a1.b_off); ad.kp2 = a1.Kp;
+      if (!a0.has_bias || !a1.has_bias) throw SpkError(SPK_E_WEIGHTS, p + ": AFF convs without bias");
+      const double bytes = 4.0 * ad.M * (3.0 * C) + 4.0 * ((double)a0.N * a0.K + (double)a1.N * a1.K);
+      const Buf xb = x.buf, yb = y.buf, ob = out.buf;
+      b.step(p + ".aff", [ad, xb, yb, ob](const Ctx& c) mutable {
+        ad.x = c.resolve(xb);
+        ad.y = c.resolve(yb);
+        ad.out = c.resolve(ob);
+        return launch_aff_x3(ad, c.stream);
+      }, aff_x3_kernel_name(mid.n_phys), bytes);
       return;
     }
     b.macs_per_utt += m0;

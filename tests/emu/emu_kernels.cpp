@@ -18,6 +18,7 @@
 #include "../../include/spk_hip.h"
 #include "../../3d-speaker_amd/csrc/fbank.h"
 #include "../../3d-speaker_amd/csrc/misc.h"
+#include "../../3d-speaker_amd/csrc/aff.h"
 
 namespace spk {
 
@@ -92,6 +93,34 @@ hipError_t launch_conv(const ConvDesc& d, hipStream_t) {
 }
 
 std::string conv_kernel_name(const ConvDesc&) { return "emu_conv"; }
+
+// fused AFF (aff.hip contract): h = SiLU(W1 [x|y] + b1), z = W2 h + b2,
+// out = x (1 + tanh z) + y (1 - tanh z); fp32 weights, double accumulation
+bool aff_x3_supported(int cp, int nmid) { return (nmid == 32 || nmid == 64) && cp % 8 == 0 && cp >= 8 && cp <= 208; }
+std::string aff_x3_kernel_name(int nmid) { return "emu_aff<" + std::to_string(nmid / 32) + ">"; }
+hipError_t launch_aff_x3(const AffDesc& a, hipStream_t) {
+  if (!aff_x3_supported(a.cp, a.nmid) || a.kp1 < 2 * a.cp || a.kp2 < a.nmid) return hipErrorInvalidValue;
+  std::vector<double> h(a.nmid);
+  for (int m = 0; m < a.M; ++m) {
+    const float* x = a.x + (size_t)m * a.ldx;
+    const float* y = a.y + (size_t)m * a.ldy;
+    for (int j = 0; j < a.nmid; ++j) {
+      double acc = a.b1[j];
+      const float* w = a.w1 + (size_t)j * a.kp1;
+      for (int k = 0; k < a.cp; ++k) acc += (double)w[k] * x[k] + (double)w[a.cp + k] * y[k];
+      const float v = (float)acc;
+      h[j] = v / (1.0f + std::exp(-v));
+    }
+    for (int n = 0; n < a.cp; ++n) {
+      double acc = a.b2[n];
+      const float* w = a.w2 + (size_t)n * a.kp2;
+      for (int j = 0; j < a.nmid; ++j) acc += (double)w[j] * h[j];
+      const float t = 1.0f + std::tanh((float)acc);
+      a.out[(size_t)m * a.ldo + n] = x[n] * t + y[n] * (2.0f - t);
+    }
+  }
+  return hipSuccess;
+}
 
 // the emulated GEMM reads the fp32 weights; the split planes are not needed on the host
 hipError_t launch_split_f16(const float*, uint16_t*, uint16_t*, size_t, hipStream_t) { return hipSuccess; }
