@@ -252,6 +252,11 @@ conv3x3_halo_persistent_kernel(const ConvDesc d) {
   if (t < ntiles) pf_store();
   __syncthreads();
 
+  f32x4 bias4 = {0.f, 0.f, 0.f, 0.f};               // loaded once: see epilogue_tiles pre_bias
+  {
+    const int n = (lane & 7) * 4;
+    if (d.bias && n < d.N) bias4 = *reinterpret_cast<const f32x4*>(d.bias + n);
+  }
   const int p_own = wave * 32 + li;                 // this lane's A row (pixel of the tile)
   const int abase = ((p_own / TW) * HW + (p_own % TW)) * C::CS + lh * C::HC;
   const int bbase = li * C::CS + lh * C::HC;
@@ -282,7 +287,7 @@ conv3x3_halo_persistent_kernel(const ConvDesc d) {
         const int p = wave * 32 + r;
         const int gy = y0 + p / TW, gx = x0 + p % TW;
         return (gy < H && gx < W) ? (img * H + gy) * W + gx : -1;
-      });
+      }, &bias4);
     }
     __syncthreads();                                // epilogue LDS reads done
     if (tn < ntiles) pf_store();
@@ -406,6 +411,13 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
   if (t < ntiles) pf_store();
   __syncthreads();
 
+  // the epilogue's bias quad, loaded once (see epilogue_tiles: with the next tile's halo in
+  // flight, a per-tile bias load would wait for the whole prefetch)
+  f32x4 bias4 = {0.f, 0.f, 0.f, 0.f};
+  {
+    const int n = n0 + (lane & 7) * 4;
+    if (d.bias && n < d.N) bias4 = *reinterpret_cast<const f32x4*>(d.bias + n);
+  }
   const int p_own = wave * 32 + li;
   const int abase = ((p_own / TW) * HW + (p_own % TW)) * C::ROW + 8 * lh;
   const int bbase = li * C::ROW + 8 * lh;
@@ -442,7 +454,7 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
         const int p = wave * 32 + r;
         const int gy = y0 + p / TW, gx = x0 + p % TW;
         return (gy < H && gx < W) ? (img * H + gy) * W + gx : -1;
-      });
+      }, &bias4);
 #else
       if (acc[0][0][0] == 12345.f) d.out[img + y0 + x0] = 1.f;
 #endif

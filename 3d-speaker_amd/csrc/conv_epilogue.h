@@ -51,9 +51,13 @@ __device__ __forceinline__ float epilogue_elem(const ConvDesc& d, int m, int n, 
 // row m of the wave's local row r (0 .. 32*TM-1), or -1 when it is outside the output.
 // LEAN = true compiles only the common-case path (bias / residual / act / post-affine,
 // float4-aligned, no split-K); the caller guarantees those conditions on the host.
+// `pre_bias` (optional, fast path): the lane's bias quads per tile, loaded by the caller
+// ahead of time.  A persistent kernel with the next tile's loads in flight must pass it:
+// vmcnt retires loads in order, so a bias load issued here would wait for all of them.
 template <int TM, int TN, bool LEAN = false, class RowMap>
 __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f32x16 (&acc)[TM][TN], int wave,
-                                               int lane, int nwave, int M, RowMap rowmap) {
+                                               int lane, int nwave, int M, RowMap rowmap,
+                                               const f32x4* pre_bias = nullptr) {
   const int li = lane & 31, lh = lane >> 5;
   // one 32x32 accumulator tile at a time through a per-wave LDS slab:
   // registers -> LDS in the MFMA C layout (col = lane&31, row = (r&3)+8(r>>2)+4(lane>>5)),
@@ -100,7 +104,8 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
         const int n = nwave + j * 32 + c4;
         if (n >= d.N) continue;
         f32x4 bias = {0.f, 0.f, 0.f, 0.f}, ps = {1.f, 1.f, 1.f, 1.f}, pt = {0.f, 0.f, 0.f, 0.f};
-        if (d.bias) bias = *reinterpret_cast<const f32x4*>(d.bias + n);
+        if (pre_bias) bias = pre_bias[tile];
+        else if (d.bias) bias = *reinterpret_cast<const f32x4*>(d.bias + n);
         if (d.post_scale) {
           ps = *reinterpret_cast<const f32x4*>(d.post_scale + n);
           pt = *reinterpret_cast<const f32x4*>(d.post_shift + n);

@@ -119,9 +119,9 @@ pw_gemm_x3_kernel(const ConvDesc d) {
   const float ps = (nok && d.post_scale) ? d.post_scale[n] : 1.f;
   const float pt = (nok && d.post_scale) ? d.post_shift[n] : 0.f;
 
-  auto tile = [&](int mt) {
-    // residual of this tile: in flight during the MFMAs
-    float res[16];
+  // residual of a tile: requested BEFORE the A prefetch of tile i+2 -- vmcnt retires
+  // loads in order, so the epilogue's wait for it then does not also wait for the prefetch
+  auto load_res = [&](int mt, float (&res)[16]) {
     const int mbase = mt * C::BM + wm * 32 + 4 * lh;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -129,6 +129,9 @@ pw_gemm_x3_kernel(const ConvDesc d) {
       m = m < M ? m : M - 1;
       res[r] = d.res ? d.res[(size_t)m * d.ldr + (nok ? n : 0)] : 0.f;
     }
+  };
+  auto tile = [&](int mt, const float (&res)[16]) {
+    const int mbase = mt * C::BM + wm * 32 + 4 * lh;
     f32x16 acc, accx;
 #pragma unroll
     for (int r = 0; r < 16; ++r) { acc[r] = 0.f; accx[r] = 0.f; }
@@ -165,14 +168,17 @@ pw_gemm_x3_kernel(const ConvDesc d) {
   if (ntiles > 0) store_a(set0);
   __syncthreads();
   for (int i = 0; i < ntiles; i += 2) {
+    float res[16];
+    load_res(mt_of(i), res);
     if (i + 2 < ntiles) load_a(mt_of(i + 2), set0);       // set 0 was staged at the end of i-1
-    tile(mt_of(i));
+    tile(mt_of(i), res);
     __syncthreads();
     if (i + 1 >= ntiles) break;
     store_a(set1);
     __syncthreads();
+    load_res(mt_of(i + 1), res);
     if (i + 3 < ntiles) load_a(mt_of(i + 3), set1);
-    tile(mt_of(i + 1));
+    tile(mt_of(i + 1), res);
     __syncthreads();
     if (i + 2 < ntiles) store_a(set0);
     __syncthreads();
