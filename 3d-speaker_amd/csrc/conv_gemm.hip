@@ -188,7 +188,7 @@ struct X3Cfg {
 };
 
 template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE, bool BUF>
-__global__ void __launch_bounds__(64 * WM * WN, 1)
+__global__ void __launch_bounds__(64 * WM * WN, (BM * BN <= 128 * 128) ? 4 : 1)
 conv_gemm_x3_kernel(const ConvDesc d) {
   using C = X3Cfg<BM, BN, WM, WN>;
   constexpr int BK = C::BK, TM = C::TM, TN = C::TN, RPP = C::RPP, AROWS = C::AROWS;
