@@ -15,7 +15,9 @@
 // 32t + 16s + 4h + {0..3} and 32t + 16s + 8 + 4h + {0..3}, and its W2 fragments are read in
 // the same order.  Stage 1 uses the k permutation of the conv GEMM (lane half h owns
 // k0 + 16h .. +15 of a 32-deep step, the two 16-deep MFMA steps take 8 each), so every lane
-// reads 64 contiguous bytes of its pixel's [x | y] row per step.
+// reads 64 contiguous bytes of its pixel's [x | y] row per step.  The combine transposes z
+// through a per-wave LDS slab, so its x / y loads and out stores are whole 128-B row
+// segments (8 lanes per pixel row) instead of 32 rows per instruction.
 // fp16x3 as in conv_gemm.hip: hi = fp16(v), lo = fp16((v − hi)·2^11), three products.
 #include <algorithm>
 #include <cstdlib>
@@ -44,14 +46,17 @@ __device__ __forceinline__ void split8(const f32x4 a, const f32x4 b, f16x8& hi, 
 __device__ __forceinline__ f16x8 ld_h8(const uint16_t* p) { return *reinterpret_cast<const f16x8*>(p); }
 __device__ __forceinline__ f16x4 ld_h4(const uint16_t* p) { return *reinterpret_cast<const f16x4*>(p); }
 
+constexpr int SLAB_LD = 36;   // LDS row stride of the per-wave 32 x 32 transpose slab (floats)
+
 template <int MT>   // bottleneck tiles of 32 channels
 __global__ void __launch_bounds__(256) aff_x3_kernel(const AffDesc a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane & 31, lh = lane >> 5;
   const int m0 = (blockIdx.x * 4 + wave) * 32;
   if (m0 >= a.M) return;                            // wave-uniform; no block barriers below
-  const bool mok = m0 + li < a.M;
-  const int m = mok ? m0 + li : a.M - 1;            // this lane's pixel
+  extern __shared__ float aff_lds[];                // >= 4 waves x 32 x SLAB_LD floats (launch)
+  float* slab = aff_lds + wave * 32 * SLAB_LD;
+  const int m = min(m0 + li, a.M - 1);             // this lane's pixel (stage-1 B column)
   const float* xr = a.x + (size_t)m * a.ldx;
   const float* yr = a.y + (size_t)m * a.ldy;
   const int K = 2 * a.cp;
@@ -122,14 +127,15 @@ __global__ void __launch_bounds__(256) aff_x3_kernel(const AffDesc a) {
   for (int n0 = 0; n0 < a.cp; n0 += 32) {
     const int n = min(n0 + li, a.cp - 1);           // W2 row of this lane (A operand)
     const bool nok = n0 + li < a.cp;
-    // lane: pixel m, channels n0 + 8q + 4h + {0..3} in registers 4q .. 4q+3; the combine's
-    // operands are requested before the MFMAs
+    // the combine works on whole 128-B row segments (8 lanes per pixel row, 4 rows per
+    // pass): x / y of those are requested before the MFMAs
+    const int c4 = (lane & 7) * 4, cc = min(n0 + c4, a.cp - 4);
     f32x4 xv[4], yv[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int c = min(n0 + 8 * q + 4 * lh, a.cp - 4);
-      xv[q] = *reinterpret_cast<const f32x4*>(xr + c);
-      yv[q] = *reinterpret_cast<const f32x4*>(yr + c);
+      const int mq = min(m0 + q * 8 + (lane >> 3), a.M - 1);
+      xv[q] = *reinterpret_cast<const f32x4*>(a.x + (size_t)mq * a.ldx + cc);
+      yv[q] = *reinterpret_cast<const f32x4*>(a.y + (size_t)mq * a.ldy + cc);
     }
     f32x16 z, zx;
 #pragma unroll
@@ -148,21 +154,30 @@ __global__ void __launch_bounds__(256) aff_x3_kernel(const AffDesc a) {
         zx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gl[t][s], zx, 0, 0, 0);
         zx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, gh[t][s], zx, 0, 0, 0);
       }
+    // transpose through the wave's LDS slab: MFMA C layout (lane = pixel) -> rows
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      slab[li * SLAB_LD + (r & 3) + 8 * (r >> 2) + 4 * lh] = z[r] + zx[r] * (1.0f / 2048.0f);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const f32x4 bias = *reinterpret_cast<const f32x4*>(a.b2 + cc);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int c = n0 + 8 * q + 4 * lh;
-      if (!mok || c >= a.cp) continue;
-      const f32x4 bias = *reinterpret_cast<const f32x4*>(a.b2 + c);
+      const int p = q * 8 + (lane >> 3);
+      const f32x4 zq = *reinterpret_cast<const f32x4*>(slab + p * SLAB_LD + c4);
       f32x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         // x(1 + tanh z) + y(1 - tanh z) = 2(y + s(x - y)), s = sigmoid(2z): one exp + rcp
-        const float zz = z[4 * q + e] + zx[4 * q + e] * (1.0f / 2048.0f) + bias[e];
-        const float sg = __frcp_rn(1.0f + __expf(-2.0f * zz));
+        const float sg = __frcp_rn(1.0f + __expf(-2.0f * (zq[e] + bias[e])));
         o[e] = 2.0f * fmaf(sg, xv[q][e] - yv[q][e], yv[q][e]);
       }
-      *reinterpret_cast<f32x4*>(a.out + (size_t)m * a.ldo + c) = o;
+      if (m0 + p < a.M && n0 + c4 < a.cp) *reinterpret_cast<f32x4*>(a.out + (size_t)(m0 + p) * a.ldo + n0 + c4) = o;
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // slab reads done before the next chunk
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
@@ -197,7 +212,7 @@ hipError_t launch_aff_x3(const AffDesc& a, hipStream_t s) {
   // is slower again).  SPK_AFF_LDS_KB overrides it for experiments.
   static const size_t lds_pad = [] {
     const char* e = std::getenv("SPK_AFF_LDS_KB");
-    return (size_t)(e ? std::atoi(e) : 60) * 1024;
+    return std::max((size_t)(e ? std::atoi(e) : 60) * 1024, (size_t)4 * 32 * SLAB_LD * sizeof(float));
   }();
   if (a.nmid == 32) hipLaunchKernelGGL(aff_x3_kernel<1>, grid, block, lds_pad, s, a);
   else hipLaunchKernelGGL(aff_x3_kernel<2>, grid, block, lds_pad, s, a);
