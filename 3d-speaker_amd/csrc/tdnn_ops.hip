@@ -35,16 +35,16 @@ __global__ void asp_stats_kernel(const float* __restrict__ x, int B, int T, int 
        e += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(e % C), b = (int)(e / C);
     const float* p = x + (size_t)b * T * ld + c;
-    const float w = 1.0f / (float)T;
-    float mean = 0.f;
-    for (int t = 0; t < T; ++t) mean += w * p[(size_t)t * ld];
-    float q = 0.f;
+    // one Welford pass (mean, M2) instead of two passes over x; var = M2 / T
+    float mean = 0.f, m2 = 0.f;
     for (int t = 0; t < T; ++t) {
-      const float d = p[(size_t)t * ld] - mean;
-      q += w * d * d;
+      const float xv = p[(size_t)t * ld];
+      const float d = xv - mean;
+      mean += d / (float)(t + 1);
+      m2 += d * (xv - mean);
     }
     out[(size_t)b * 2 * C + c] = mean;
-    out[(size_t)b * 2 * C + C + c] = sqrtf(fmaxf(q, eps));
+    out[(size_t)b * 2 * C + C + c] = sqrtf(fmaxf(m2 / (float)T, eps));
   }
 }
 
@@ -55,20 +55,26 @@ __global__ void attn_pool_kernel(const float* __restrict__ logit, int ldl, const
     const int c = (int)(e % C), b = (int)(e / C);
     const float* l = logit + (size_t)b * T * ldl + c;
     const float* p = x + (size_t)b * T * ldx + c;
-    float mx = -INFINITY;
-    for (int t = 0; t < T; ++t) mx = fmaxf(mx, l[(size_t)t * ldl]);
-    float den = 0.f;
-    for (int t = 0; t < T; ++t) den += __expf(l[(size_t)t * ldl] - mx);
-    const float inv = 1.0f / den;
-    float mean = 0.f;
-    for (int t = 0; t < T; ++t) mean += (__expf(l[(size_t)t * ldl] - mx) * inv) * p[(size_t)t * ldx];
-    float q = 0.f;
+    // one pass: online softmax (running max, weights rescaled when it moves) fused with a
+    // weighted Welford update of mean and M2 = sum w (x - mean)^2, so logits and x are read
+    // once instead of four and two times; var = M2 / sum w (ECAPA_TDNN.py:276-287)
+    float mx = -INFINITY, sw = 0.f, mean = 0.f, m2 = 0.f;
     for (int t = 0; t < T; ++t) {
-      const float d = p[(size_t)t * ldx] - mean;
-      q += (__expf(l[(size_t)t * ldl] - mx) * inv) * d * d;
+      const float lv = l[(size_t)t * ldl], xv = p[(size_t)t * ldx];
+      if (lv > mx) {
+        const float sc = __expf(mx - lv);           // 0 on the first sample
+        sw *= sc;
+        m2 *= sc;
+        mx = lv;
+      }
+      const float w = __expf(lv - mx);
+      sw += w;
+      const float d = xv - mean;
+      mean += d * (w / sw);
+      m2 += w * d * (xv - mean);
     }
     out[(size_t)b * 2 * C + c] = mean;
-    out[(size_t)b * 2 * C + C + c] = sqrtf(fmaxf(q, eps));
+    out[(size_t)b * 2 * C + C + c] = sqrtf(fmaxf(m2 / sw, eps));
   }
 }
 
