@@ -51,6 +51,9 @@ struct ConvDesc {
   const float* bias = nullptr; // [N] or null
   const float* rowbias = nullptr; int rowbias_ld = 0;  // per-image bias [nimg][rowbias_ld] (ECAPA ASP context)
   float* out = nullptr; int ldo = 0;
+  // planar output slices (Res2Net conv1 -> T1): column n goes to plane n / osplit at
+  // offset n % osplit of a [M][ldo] plane, planes oplane floats apart (0: one dense buffer)
+  int osplit = 0; long long oplane = 0;
   int act = ACT_NONE;
   int act2 = ACT_NONE;         // applied after the post-affine (ECAPA ASP: BN then tanh)
   const float* res = nullptr; int ldr = 0;             // added before act
@@ -70,6 +73,13 @@ struct ConvDesc {
 __device__ __forceinline__ int xcd_remap(int orig, int nblk) {
   const int q = nblk / 8, r = nblk % 8, xcd = orig % 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+// address of output element (m, n) (4 consecutive columns never straddle a plane:
+// osplit is a multiple of 4, checked on the host)
+__host__ __device__ inline float* out_at(const ConvDesc& d, int m, int n) {
+  if (d.osplit) return d.out + (size_t)(n / d.osplit) * d.oplane + (size_t)m * d.ldo + n % d.osplit;
+  return d.out + (size_t)m * d.ldo + n;
 }
 
 // true when output row m is past its image's valid length (ragged batches)

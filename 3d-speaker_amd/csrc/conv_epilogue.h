@@ -103,6 +103,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
         const int i = tile / TN, j = tile % TN;
         const int n = nwave + j * 32 + c4;
         if (n >= d.N) continue;
+        float* const ocol = out_at(d, 0, n);   // plane / column split once per tile, not per row
         f32x4 bias = {0.f, 0.f, 0.f, 0.f}, ps = {1.f, 1.f, 1.f, 1.f}, pt = {0.f, 0.f, 0.f, 0.f};
         if (pre_bias) bias = pre_bias[tile];
         else if (d.bias) bias = *reinterpret_cast<const f32x4*>(d.bias + n);
@@ -124,7 +125,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
             o[e] = apply_act(x, d.act2);
           }
           if (row_masked(d, m)) o = f32x4{0.f, 0.f, 0.f, 0.f};
-          *reinterpret_cast<f32x4*>(d.out + (size_t)m * d.ldo + n) = o;
+          *reinterpret_cast<f32x4*>(ocol + (size_t)m * d.ldo) = o;
         }
       }
       return;
@@ -154,6 +155,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
         const int i = tile / TN, j = tile % TN;
         const int n = nwave + j * 32 + c4;
         if (n >= d.N) continue;
+        float* const ocol = out_at(d, 0, n);
         f32x4 bias = {0.f, 0.f, 0.f, 0.f};
         if (d.bias) bias = *reinterpret_cast<const f32x4*>(d.bias + n);
         const float* ct = cw + tile * 1024;
@@ -169,7 +171,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
             o[e] = xa[tile][q][e] * t + ya[tile][q][e] * (2.0f - t);
           }
           if (row_masked(d, m)) o = f32x4{0.f, 0.f, 0.f, 0.f};
-          *reinterpret_cast<f32x4*>(d.out + (size_t)m * d.ldo + n) = o;
+          *reinterpret_cast<f32x4*>(ocol + (size_t)m * d.ldo) = o;
         }
       }
       return;
@@ -185,6 +187,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
       if (vec) {
         const int c4 = (lane & 7) * 4;
         const int n = nbase + c4;
+        float* const ocol = out_at(d, 0, n < d.N ? n : 0);
         f32x4 bias = {0.f, 0.f, 0.f, 0.f}, ps = {1.f, 1.f, 1.f, 1.f}, pt = {0.f, 0.f, 0.f, 0.f};
         if (!part && n < d.N) {
           if (d.bias) bias = *reinterpret_cast<const f32x4*>(d.bias + n);
@@ -241,11 +244,12 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
               }
             }
             if (row_masked(d, m)) o = f32x4{0.f, 0.f, 0.f, 0.f};
-            *reinterpret_cast<f32x4*>(d.out + (size_t)m * d.ldo + n) = o;
+            *reinterpret_cast<f32x4*>(ocol + (size_t)m * d.ldo) = o;
           }
         }
       } else {
         const int n = nbase + li;
+        float* const ocol = out_at(d, 0, n < d.N ? n : 0);
 #pragma unroll 2
         for (int q = 0; q < 16; ++q) {
           const int rl = 2 * q + lh;
@@ -253,7 +257,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
           if (m >= 0 && m < M && n < d.N) {
             const float v = ct[rl * 32 + li];
             if (part) part[(size_t)m * d.N + n] = v;
-            else d.out[(size_t)m * d.ldo + n] = epilogue_elem(d, m, n, v);
+            else ocol[(size_t)m * d.ldo] = epilogue_elem(d, m, n, v);
           }
         }
       }

@@ -349,7 +349,7 @@ __global__ void splitk_reduce_kernel(const ConvDesc d, int M) {
     const int m = e / d.N, n = e % d.N;
     float v = 0.f;
     for (int z = 0; z < d.ksplit; ++z) v += d.partial[(size_t)z * total + e];
-    d.out[(size_t)m * d.ldo + n] = epilogue_elem(d, m, n, v);
+    *out_at(d, m, n) = epilogue_elem(d, m, n, v);
   }
 }
 
@@ -468,7 +468,7 @@ bool conv_use_x3() { return use_x3(); }
 
 hipError_t launch_conv(const ConvDesc& d, hipStream_t s) {
   // host-side shape checks: every float4 access must stay aligned and in range
-  if (d.s0.cin % 4 || d.s0.ld % 4 || (d.s0.p2 && d.s0.ld2 % 4) || d.Kp % KP_ALIGN || d.ldo < d.N ||
+  if (d.s0.cin % 4 || d.s0.ld % 4 || (d.s0.p2 && d.s0.ld2 % 4) || d.Kp % KP_ALIGN || (d.osplit ? (d.osplit % 4 || d.ldo < d.osplit) : d.ldo < d.N) ||
       (d.s1.p && (d.s1.cin % 4 || d.s1.ld % 4)) || d.N <= 0 || d.nimg <= 0 || d.Ho <= 0 || d.Wo <= 0 ||
       (reinterpret_cast<uintptr_t>(d.s0.p) & 15) || (reinterpret_cast<uintptr_t>(d.w) & 15) ||
       d.K > d.Kp || (d.ksplit > 1 && !d.partial))

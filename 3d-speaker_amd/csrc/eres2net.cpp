@@ -8,7 +8,10 @@
 //   * every block output is dense C = planes*expansion;
 //   * the conv1 output "T1" and the Res2Net concat buffer "CAT" hold `scale` slices of
 //     `width` channels, each zero-padded to a multiple of 4 (width 26 -> 28) so float4
-//     loads stay aligned; torch.split / torch.cat are just slice offsets;
+//     loads stay aligned; torch.split / torch.cat are just slice offsets.  T1 is planar
+//     (slice i is its own dense [px][wp] plane, written by conv1's split epilogue): the 3x3
+//     conv of a slice then reads whole cache lines instead of 112 of every 224 bytes;
+//     CAT stays interleaved, the K operand conv3 reads in one piece;
 //   * conv3 + bn3 + shortcut conv + its BN + residual add + Hardtanh are ONE GEMM: the
 //     shortcut input is K-concatenated as a second operand with its own stride;
 //   * `sp + spx` is fused into the 3x3 conv's operand load; AFF is two GEMMs, the second
@@ -133,6 +136,7 @@ struct ERes2Builder {
     const ChanMap sl = ChanMap::slices(width, scale);
     const int wp = sl.n_phys / scale;
     const int ldt = sl.n_phys;
+    const size_t t1_plane = (size_t)b.B * Ho * Wo * wp;   // floats per T1 slice plane
     const ChanMap xin = ChanMap::dense(x.C);
     const double px = (double)Ho * Wo;
 
@@ -143,13 +147,14 @@ struct ERes2Builder {
       ConvDesc d;
       d.nimg = b.B; d.Ho = Ho; d.Wo = Wo;
       d.s0 = src_of(nullptr, x, x.C, 1, stride, 0);
-      d.ldo = ldt; d.act = ACT_HTANH;
+      d.ldo = wp; d.osplit = wp; d.oplane = (long long)t1_plane;
+      d.act = ACT_HTANH;
       Builder::ConvIO io; io.s0 = x.buf; io.out = T1;
       b.conv(p + ".conv1", d, c1, io);
     }
     const T4 cat{CAT, ldt, Ho, Wo, ldt};
     for (int i = 0; i < scale; ++i) {
-      T4 in{T1.at((size_t)i * wp), ldt, Ho, Wo, wp};
+      T4 in{T1.at((size_t)i * t1_plane), wp, Ho, Wo, wp};
       Buf addend;
       int add_ld = 0;
       if (i > 0) {

@@ -115,6 +115,7 @@ pw_gemm_x3_kernel(const ConvDesc d) {
 
   const int n = n0 + wn * 32 + li;                         // this lane's output column
   const bool nok = n < d.N;
+  float* const ocol = out_at(d, 0, nok ? n : 0);           // its plane / offset, once
   const float bias = (nok && d.bias) ? d.bias[n] : 0.f;
   const float ps = (nok && d.post_scale) ? d.post_scale[n] : 1.f;
   const float pt = (nok && d.post_scale) ? d.post_shift[n] : 0.f;
@@ -154,7 +155,7 @@ pw_gemm_x3_kernel(const ConvDesc d) {
         if (m >= M) continue;
         float v = apply_act(acc[r] + accx[r] * (1.0f / 2048.0f) + bias + res[r], d.act);
         if (d.post_scale) v = v * ps + pt;
-        d.out[(size_t)m * d.ldo + n] = row_masked(d, m) ? 0.f : apply_act(v, d.act2);
+        ocol[(size_t)m * d.ldo] = row_masked(d, m) ? 0.f : apply_act(v, d.act2);
       }
     }
   };

@@ -52,7 +52,7 @@ static float epilogue(const ConvDesc& d, int m, int n, float v) {
 }
 
 hipError_t launch_conv(const ConvDesc& d, hipStream_t) {
-  if (d.s0.cin % 4 || d.s0.ld % 4 || d.Kp % 16 || d.ldo < d.N || d.K > d.Kp) return hipErrorInvalidValue;
+  if (d.s0.cin % 4 || d.s0.ld % 4 || d.Kp % 16 || (d.osplit ? (d.osplit % 4 || d.ldo < d.osplit) : d.ldo < d.N) || d.K > d.Kp) return hipErrorInvalidValue;
   const int M = d.nimg * d.Ho * d.Wo;
   const int K0 = d.s0.kh * d.s0.kw * d.s0.cin;
   std::vector<float> a(d.Kp);
@@ -86,7 +86,7 @@ hipError_t launch_conv(const ConvDesc& d, hipStream_t) {
       const float* w = d.w + (size_t)n * d.Kp;
       double acc = 0.0;
       for (int k = 0; k < d.Kp; ++k) acc += (double)a[k] * w[k];
-      d.out[(size_t)m * d.ldo + n] = epilogue(d, m, n, (float)acc);
+      *out_at(d, m, n) = epilogue(d, m, n, (float)acc);
     }
   }
   return hipSuccess;
