@@ -72,13 +72,13 @@ tstp_kernel(const float* __restrict__ x, int B, int H, int W, int C, int ld, flo
     const int h = (int)((e / C) % H);
     const int b = (int)(e / ((long long)C * H));
     const float* p = x + ((size_t)(b * H + h) * W) * ld + c;
-    float s = 0.f;
-    for (int t = 0; t < W; ++t) s += p[(size_t)t * ld];
-    const float mean = s / (float)W;
-    float q = 0.f;
+    // one Welford pass (mean, M2): the activation is read once, not twice
+    float mean = 0.f, q = 0.f;
     for (int t = 0; t < W; ++t) {
-      const float dlt = p[(size_t)t * ld] - mean;
-      q = fmaf(dlt, dlt, q);
+      const float v = p[(size_t)t * ld];
+      const float dlt = v - mean;
+      mean += dlt / (float)(t + 1);
+      q = fmaf(dlt, v - mean, q);
     }
     const float var = q / (float)(unbiased ? W - 1 : W);
     float* o = out + (size_t)b * 2 * H * C;

@@ -124,13 +124,12 @@ __global__ void stats_pool_kernel(const float* __restrict__ x, int B, int T, int
     const int c = (int)(e % C), b = (int)(e / C);
     const int Tb = vlen ? vlen[b] : T;
     const float* p = x + (size_t)b * T * ld + c;
-    float s = 0.f;
-    for (int t = 0; t < Tb; ++t) s += p[(size_t)t * ld];
-    const float mean = s / (float)Tb;
-    float q = 0.f;
+    float mean = 0.f, q = 0.f;                       // one Welford pass (mean, M2)
     for (int t = 0; t < Tb; ++t) {
-      const float d = p[(size_t)t * ld] - mean;
-      q += d * d;
+      const float v = p[(size_t)t * ld];
+      const float d = v - mean;
+      mean += d / (float)(t + 1);
+      q += d * (v - mean);
     }
     out[(size_t)b * 2 * C + c] = mean;
     out[(size_t)b * 2 * C + C + c] = sqrtf(q / (float)(Tb - 1));
