@@ -18,6 +18,22 @@ __device__ __forceinline__ float apply_act(float v, int act) {
   }
 }
 
+// fp16x3 split of a staged fp32 quad (conv_gemm.hip "fp16x3"): hi = fp16(v) and
+// lo = fp16((v - hi) * 2^11), with packed round-toward-zero conversions (two values per
+// instruction, already packed; |v - hi| < ulp(hi) and lo keeps the remainder to 2^-22).
+typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void split_x3(const f32x4 v, h16x4& h, h16x4& l) {
+  typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+  const h16x2 h01 = __builtin_bit_cast(h16x2, __builtin_amdgcn_cvt_pkrtz(v[0], v[1]));
+  const h16x2 h23 = __builtin_bit_cast(h16x2, __builtin_amdgcn_cvt_pkrtz(v[2], v[3]));
+  const h16x2 l01 = __builtin_bit_cast(
+      h16x2, __builtin_amdgcn_cvt_pkrtz((v[0] - (float)h01[0]) * 2048.0f, (v[1] - (float)h01[1]) * 2048.0f));
+  const h16x2 l23 = __builtin_bit_cast(
+      h16x2, __builtin_amdgcn_cvt_pkrtz((v[2] - (float)h23[0]) * 2048.0f, (v[3] - (float)h23[1]) * 2048.0f));
+  h = h16x4{h01[0], h01[1], h23[0], h23[1]};
+  l = h16x4{l01[0], l01[1], l23[0], l23[1]};
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();

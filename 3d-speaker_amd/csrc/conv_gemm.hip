@@ -254,18 +254,10 @@ conv_gemm_x3_kernel(const ConvDesc d) {
 #pragma unroll
     for (int r = 0; r < AROWS; ++r) {
       const f32x4 v = al.value(st.a, r);
-      // packed round-toward-zero conversions: two values per instruction, already packed
-      // (RTZ hi leaves |v - hi| < ulp(hi); lo still carries it to 2^-22).  Measured: -0.3 ms
-      // per ERes2NetV2 forward against per-element round-to-nearest conversions.
-      typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-      const f16x2 h01 = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz(v[0], v[1]));
-      const f16x2 h23 = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz(v[2], v[3]));
-      const f16x2 l01 = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz((v[0] - (float)h01[0]) * 2048.0f,
-                                                                            (v[1] - (float)h01[1]) * 2048.0f));
-      const f16x2 l23 = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz((v[2] - (float)h23[0]) * 2048.0f,
-                                                                            (v[3] - (float)h23[1]) * 2048.0f));
-      const f16x4 h = {h01[0], h01[1], h23[0], h23[1]};
-      const f16x4 l = {l01[0], l01[1], l23[0], l23[1]};
+      // packed round-toward-zero split (conv_epilogue.h split_x3; measured -0.3 ms per
+      // ERes2NetV2 forward against per-element round-to-nearest conversions)
+      f16x4 h, l;
+      split_x3(v, h, l);
       const int off = (row0 + RPP * r) * C::LROW + kq * 4;
       *reinterpret_cast<f16x4*>(ahi + off) = h;
       *reinterpret_cast<f16x4*>(alo + off) = l;
