@@ -386,6 +386,14 @@ Cfg select_cfg(const ConvDesc& d) {
     if (t == 1) return {256, 128, 32, 4, 2};
     if (t == 2) return {128, 256, 32, 2, 4};
     if (t == 3) return {128, 128, 32, 2, 4};
+    // measured per layer (tools/gpu_ab.sh over SPK_X3_TILE): the K-concatenated shortcut
+    // GEMMs (conv3 + shortcut, AFF cat) run best on 128x256 tiles; residual epilogues with
+    // K <= 512 on 128x128 tiles, two blocks per CU, so one block's epilogue round trips
+    // overlap the other's main loop (ERes2Net-large layer3 conv3 0.68 -> 0.52 ms)
+    const bool s1 = d.s1.p != nullptr || d.s1.cin > 0;
+    const bool res = d.res != nullptr || d.ldr > 0;
+    if (s1 && d.Kp >= 256 && d.N % 256 == 0) return {128, 256, 32, 2, 4};
+    if (res && d.Kp >= 256 && d.Kp <= 512) return {128, 128, 32, 2, 4};
     // deep K: bigger tiles halve the L2 traffic per FLOP (measured per layer)
     if (d.Kp >= 1024 && d.N >= 512 && d.N % 256 == 0) return {128, 256, 32, 2, 4};
     if (d.Kp >= 256) return {256, 128, 32, 4, 2};
