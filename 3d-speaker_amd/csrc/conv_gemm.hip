@@ -393,6 +393,8 @@ Cfg select_cfg(const ConvDesc& d) {
     const bool s1 = d.s1.p != nullptr || d.s1.cin > 0;
     const bool res = d.res != nullptr || d.ldr > 0;
     if (s1 && d.Kp >= 256 && d.N % 256 == 0) return {128, 256, 32, 2, 4};
+    // CAM++ dense layers (BN-ReLU applied in the loader, N = 128): 128x256 as well (-6 %)
+    if (d.s0.pre_scale && d.Kp >= 256) return {128, 256, 32, 2, 4};
     if (res && d.Kp >= 256 && d.Kp <= 512) return {128, 128, 32, 2, 4};
     // deep K: bigger tiles halve the L2 traffic per FLOP (measured per layer)
     if (d.Kp >= 1024 && d.N >= 512 && d.N % 256 == 0) return {128, 256, 32, 2, 4};
