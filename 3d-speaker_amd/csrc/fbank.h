@@ -4,17 +4,20 @@
 
 namespace spk {
 
+// Constant tables in double precision: the kernel computes the whole front end in fp64
+// (feature noise is amplified ~60x into the embedding, so the fp32 FFT
+// noise of a direct implementation would eat most of the 1e-4 embedding budget).
 struct FbankTables {
-  float window[400];        // Povey window hann(400, periodic=False)^0.85
-  float2 twiddle[256];      // exp(-2 pi i k / 512)
+  double window[400];       // Povey window hann(400, periodic=False)^0.85
+  double2 twiddle[512];     // exp(-2 pi i j / 512), j = 0..511
   int mel_start[128];       // first FFT bin of filter m
   int mel_len[128];         // number of bins with non-zero weight
   int mel_off[128];         // offset of its weights in mel_w
-  float mel_w[4096];
+  double mel_w[4096];
 };
 
-// Host-side construction (double precision, rounded once to float).  Returns the number
-// of mel weights used; -1 if n_mels is unsupported.
+// Host-side construction (double precision).  Returns the number of mel weights used;
+// -1 if n_mels is unsupported.
 int build_fbank_tables(FbankTables* t, int n_mels, double sample_rate);
 
 // t_max > 0: utterance u is written at rows [u * t_max, u * t_max + frames_u), the rest of

@@ -1,4 +1,4 @@
-// Host construction of the Fbank constant tables (double precision, rounded once).
+// Host construction of the Fbank constant tables (double precision, kept in double).
 // Window: torchaudio _feature_window_function(POVEY) = hann_window(400, periodic=False)^0.85.
 // Mel bank: torchaudio get_mel_banks (mel = 1127 ln(1 + f/700), low 20 Hz, high = Nyquist,
 // 512-point FFT, vtln_warp = 1), the Nyquist column is zero so only bins 0..255 carry weight.
@@ -12,11 +12,11 @@ int build_fbank_tables(FbankTables* t, int n_mels, double sample_rate) {
   const double pi = 3.14159265358979323846;
   for (int i = 0; i < 400; ++i) {
     const double h = 0.5 - 0.5 * std::cos(2.0 * pi * i / 399.0);
-    t->window[i] = (float)std::pow(h, 0.85);
+    t->window[i] = std::pow(h, 0.85);
   }
-  for (int k = 0; k < 256; ++k) {
+  for (int k = 0; k < 512; ++k) {
     const double a = -2.0 * pi * k / 512.0;
-    t->twiddle[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+    t->twiddle[k] = make_double2(std::cos(a), std::sin(a));
   }
   auto mel = [](double f) { return 1127.0 * std::log(1.0 + f / 700.0); };
   const double nyq = 0.5 * sample_rate;
@@ -43,7 +43,7 @@ int build_fbank_tables(FbankTables* t, int n_mels, double sample_rate) {
       const double mb = mel(bin_w * b);
       const double w = std::fmax(0.0, std::fmin((mb - left) / (center - left), (right - mb) / (right - center)));
       if (off >= 4096) return -1;
-      t->mel_w[off++] = (float)w;
+      t->mel_w[off++] = w;
     }
   }
   return off;

@@ -53,5 +53,5 @@ def test_infer_sv_batch_matches_oracle(tmp_path, fmt):
     assert sorted(got) == sorted(ref)
     for k in ref:
         assert got[k].shape == (192,)
-        # end to end includes the fp32 FFT noise of the Fbank (tests/test_gpu_fbank.py)
-        assert helpers.rel_err(got[k][None], ref[k][None]).max() < 5e-4, k
+        # end to end from wav at the north-star bar (the GPU Fbank computes in fp64)
+        assert helpers.rel_err(got[k][None], ref[k][None]).max() < 1e-4, k

@@ -42,8 +42,8 @@ def test_diarization_matches_oracle(tmp_path):
     chunks, emb_ref = _oracle_segments(diar, wav)
     emb = diar.do_emb_extraction(chunks, torch.from_numpy(wav)[None])
     assert emb.shape == emb_ref.shape and len(chunks) > 10
-    # end to end incl. Fbank fp32 FFT noise (tests/test_gpu_fbank.py)
-    assert helpers.rel_err(emb, emb_ref).max() < 5e-4
+    # end to end from wav at the north-star bar (fp64 GPU Fbank, tests/test_gpu_fbank.py)
+    assert helpers.rel_err(emb, emb_ref).max() < 1e-4
     # same clustering decisions on the oracle embeddings (host cosine in fp64)
     S = cluster._host_cosine(emb_ref, emb_ref).astype(np.float32)
     lab = cluster.ahc_labels(S, 0.3)

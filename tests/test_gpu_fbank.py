@@ -13,9 +13,11 @@ pytestmark = pytest.mark.gpu
 
 def _check(feat, ref):
     err = np.abs(feat - ref)
-    # fp32 FFT noise is ~1e-7 of the frame energy: visible only in near-silent mel bands
-    assert err.max() < 2e-3, err.max()
-    assert np.median(err) < 2e-6, np.median(err)
+    # the kernel computes in fp64 like the oracle: what is left is the fp32 rounding of the
+    # stored log-mel (half an ulp of |x| <= 16 is 9.5e-7) plus, with mean_nor, the rounding
+    # of the normalised value
+    assert err.max() < 5e-6, err.max()
+    assert np.median(err) < 1e-6, np.median(err)
 
 
 @pytest.mark.parametrize('mean_nor', [False, True])
