@@ -57,6 +57,10 @@ void build_ecapa(Builder& b, int T) {
   const int catC = C[1] + C[2] + C[3];
   if (catC != C[4]) throw SpkError(SPK_E_WEIGHTS, "ECAPA: mfa input must be the concatenation of the 3 blocks");
   const double Td = T;
+  // forward(x, lengths) (ECAPA_TDNN.py:430-454): the convolutions run over the whole padded
+  // [B, T] input exactly like the reference (no masking there); only the SE squeeze means
+  // and the attentive-pooling statistics are restricted to each utterance's valid frames
+  const Buf LENS = b.ragged ? Buf{Buf::LEN, 0, nullptr} : Buf{};
   int cmax = std::max(std::max(C[0], C[1]), std::max(C[2], C[3]));
 
   auto post = [&](const std::string& bn, int n) { return &m.pack_post_affine(bn, bn, ChanMap::dense(n)); };
@@ -189,7 +193,7 @@ void build_ecapa(Builder& b, int T) {
                                 {Part{q + ".conv2.conv.weight", q + ".conv2.conv.bias", "", ChanMap::dense(se), 0, 0}}, se);
       b.macs_per_utt += 2.0 * Ci * se;
       if (b.plan) {
-        b.step(q + ".mean", [=](const Ctx& c) { return launch_time_mean(c.resolve(H2), B, T, Ci, Ci, c.resolve(S), Ci, c.stream); });
+        b.step(q + ".mean", [=](const Ctx& c) { return launch_time_mean(c.resolve(H2), B, T, Ci, Ci, c.resolve(S), Ci, c.stream, c.resolve_i(LENS)); });
         ConvDesc d1;
         d1.nimg = B; d1.Ho = 1; d1.Wo = 1;
         d1.s0 = src_vec(Ci);
@@ -258,7 +262,7 @@ void build_ecapa(Builder& b, int T) {
     b.macs_per_utt += macs_ctx + macs_att + macs_conv + macs_fc;
     return;
   }
-  b.step("asp.stats", [=](const Ctx& c) { return launch_asp_stats(c.resolve(A), B, T, Cm, Cm, 1e-12f, c.resolve(MS), c.stream); });
+  b.step("asp.stats", [=](const Ctx& c) { return launch_asp_stats(c.resolve(A), B, T, Cm, Cm, 1e-12f, c.resolve(MS), c.stream, c.resolve_i(LENS)); });
   {
     ConvDesc d;
     d.nimg = B; d.Ho = 1; d.Wo = 1;
@@ -289,7 +293,8 @@ void build_ecapa(Builder& b, int T) {
     b.conv("asp.conv", d, patt2, io);
   }
   b.step("asp.pool", [=](const Ctx& c) {
-    return launch_attn_pool(c.resolve(L), Cm, c.resolve(A), Cm, B, T, Cm, 1e-12f, c.resolve(P), c.stream);
+    return launch_attn_pool(c.resolve(L), Cm, c.resolve(A), Cm, B, T, Cm, 1e-12f, c.resolve(P), c.stream,
+                            c.resolve_i(LENS));
   });
   {
     ConvDesc d;

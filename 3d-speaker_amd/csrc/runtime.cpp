@@ -255,8 +255,8 @@ Plan* get_plan(spk_model_t* h, int B, int T, bool ragged = false) {
   auto key = std::make_pair(B, ragged ? -T : T);
   auto it = h->m.plans.find(key);
   if (it != h->m.plans.end()) return it->second.get();
-  if (ragged && h->m.cfg.arch != SPK_ARCH_CAMPPLUS)
-    throw SpkError(SPK_E_UNSUPPORTED, "per-utterance lengths are implemented for CAM++ only");
+  if (ragged && h->m.cfg.arch != SPK_ARCH_CAMPPLUS && h->m.cfg.arch != SPK_ARCH_ECAPA)
+    throw SpkError(SPK_E_UNSUPPORTED, "per-utterance lengths are implemented for CAM++ and ECAPA-TDNN only");
   auto plan = std::make_unique<Plan>();
   Builder b(h->m, plan.get(), B, ragged);
   switch (h->m.cfg.arch) {

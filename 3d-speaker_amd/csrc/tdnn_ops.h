@@ -4,10 +4,13 @@
 
 namespace spk {
 
-hipError_t launch_time_mean(const float* x, int B, int T, int C, int ld, float* out, int ldo, hipStream_t s);
-hipError_t launch_asp_stats(const float* x, int B, int T, int C, int ld, float eps, float* out, hipStream_t s);
+// vlen (optional): per-utterance valid frames; the statistics cover frames [0, vlen[b])
+hipError_t launch_time_mean(const float* x, int B, int T, int C, int ld, float* out, int ldo, hipStream_t s,
+                            const int* vlen = nullptr);
+hipError_t launch_asp_stats(const float* x, int B, int T, int C, int ld, float eps, float* out, hipStream_t s,
+                            const int* vlen = nullptr);
 hipError_t launch_attn_pool(const float* logit, int ldl, const float* x, int ldx, int B, int T, int C, float eps,
-                            float* out, hipStream_t s);
+                            float* out, hipStream_t s, const int* vlen = nullptr);
 hipError_t launch_se_apply(const float* x, int ldx, const float* gate, int ldg, const float* res, int ldr, float* out,
                            int ldo, int B, int T, int C, hipStream_t s);
 // vlen (optional, ragged batches): valid frames per utterance

@@ -17,49 +17,59 @@ namespace {
 
 inline int grid_for(long long n) { return (int)std::min<long long>((n + 255) / 256, 65536); }
 
+// vlen (optional): utterance b's statistics cover frames [0, valid(b)) only -- ECAPA's
+// masked SE / ASP (ECAPA_TDNN.py:211-214, 259-270, 281-282); the host guarantees
+// 1 <= vlen[b] <= T and the kernels clamp to that range anyway
+__device__ __forceinline__ int valid_frames(const int* vlen, int b, int T) {
+  return vlen ? min(max(vlen[b], 1), T) : T;
+}
+
 __global__ void time_mean_kernel(const float* __restrict__ x, int B, int T, int C, int ld, float* __restrict__ out,
-                                 int ldo) {
+                                 int ldo, const int* __restrict__ vlen) {
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
        e += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(e % C), b = (int)(e / C);
+    const int Tb = valid_frames(vlen, b, T);
     const float* p = x + (size_t)b * T * ld + c;
     float s = 0.f;
-    for (int t = 0; t < T; ++t) s += p[(size_t)t * ld];
-    out[(size_t)b * ldo + c] = s / (float)T;
+    for (int t = 0; t < Tb; ++t) s += p[(size_t)t * ld];
+    out[(size_t)b * ldo + c] = s / (float)Tb;
   }
 }
 
 __global__ void asp_stats_kernel(const float* __restrict__ x, int B, int T, int C, int ld, float eps,
-                                 float* __restrict__ out) {
+                                 float* __restrict__ out, const int* __restrict__ vlen) {
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
        e += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(e % C), b = (int)(e / C);
+    const int Tb = valid_frames(vlen, b, T);
     const float* p = x + (size_t)b * T * ld + c;
     // one Welford pass (mean, M2) instead of two passes over x; var = M2 / T
     float mean = 0.f, m2 = 0.f;
-    for (int t = 0; t < T; ++t) {
+    for (int t = 0; t < Tb; ++t) {
       const float xv = p[(size_t)t * ld];
       const float d = xv - mean;
       mean += d / (float)(t + 1);
       m2 += d * (xv - mean);
     }
     out[(size_t)b * 2 * C + c] = mean;
-    out[(size_t)b * 2 * C + C + c] = sqrtf(fmaxf(m2 / (float)T, eps));
+    out[(size_t)b * 2 * C + C + c] = sqrtf(fmaxf(m2 / (float)Tb, eps));
   }
 }
 
 __global__ void attn_pool_kernel(const float* __restrict__ logit, int ldl, const float* __restrict__ x, int ldx, int B,
-                                 int T, int C, float eps, float* __restrict__ out) {
+                                 int T, int C, float eps, float* __restrict__ out, const int* __restrict__ vlen) {
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
        e += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(e % C), b = (int)(e / C);
+    const int Tb = valid_frames(vlen, b, T);   // masked_fill(-inf) past it: weight 0
     const float* l = logit + (size_t)b * T * ldl + c;
     const float* p = x + (size_t)b * T * ldx + c;
     // one pass: online softmax (running max, weights rescaled when it moves) fused with a
     // weighted Welford update of mean and M2 = sum w (x - mean)^2, so logits and x are read
     // once instead of four and two times; var = M2 / sum w (ECAPA_TDNN.py:276-287)
     float mx = -INFINITY, sw = 0.f, mean = 0.f, m2 = 0.f;
-    for (int t = 0; t < T; ++t) {
+    for (int t = 0; t < Tb; ++t) {
       const float lv = l[(size_t)t * ldl], xv = p[(size_t)t * ldx];
       if (lv > mx) {
         const float sc = __expf(mx - lv);           // 0 on the first sample
@@ -103,7 +113,7 @@ __global__ void cam_context_kernel(const float* __restrict__ x, int B, int T, in
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
        e += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(e % C), b = (int)(e / C);
-    const int Tb = vlen ? vlen[b] : T;
+    const int Tb = valid_frames(vlen, b, T);
     const float* p = x + (size_t)b * T * ld + c;
     float tot = 0.f;
     for (int t = 0; t < Tb; ++t) tot += p[(size_t)t * ld];
@@ -122,7 +132,7 @@ __global__ void stats_pool_kernel(const float* __restrict__ x, int B, int T, int
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
        e += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(e % C), b = (int)(e / C);
-    const int Tb = vlen ? vlen[b] : T;
+    const int Tb = valid_frames(vlen, b, T);
     const float* p = x + (size_t)b * T * ld + c;
     float mean = 0.f, q = 0.f;                       // one Welford pass (mean, M2)
     for (int t = 0; t < Tb; ++t) {
@@ -144,20 +154,24 @@ __global__ void derive_len_kernel(const int* __restrict__ in, int* __restrict__ 
 
 }  // namespace
 
-hipError_t launch_time_mean(const float* x, int B, int T, int C, int ld, float* out, int ldo, hipStream_t s) {
-  hipLaunchKernelGGL(time_mean_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, out, ldo);
+hipError_t launch_time_mean(const float* x, int B, int T, int C, int ld, float* out, int ldo, hipStream_t s,
+                            const int* vlen) {
+  hipLaunchKernelGGL(time_mean_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, out, ldo,
+                     vlen);
   return hipGetLastError();
 }
 
-hipError_t launch_asp_stats(const float* x, int B, int T, int C, int ld, float eps, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(asp_stats_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, eps, out);
+hipError_t launch_asp_stats(const float* x, int B, int T, int C, int ld, float eps, float* out, hipStream_t s,
+                            const int* vlen) {
+  hipLaunchKernelGGL(asp_stats_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, eps, out,
+                     vlen);
   return hipGetLastError();
 }
 
 hipError_t launch_attn_pool(const float* logit, int ldl, const float* x, int ldx, int B, int T, int C, float eps,
-                            float* out, hipStream_t s) {
+                            float* out, hipStream_t s, const int* vlen) {
   hipLaunchKernelGGL(attn_pool_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, logit, ldl, x, ldx, B, T, C,
-                     eps, out);
+                     eps, out, vlen);
   return hipGetLastError();
 }
 

@@ -193,6 +193,7 @@ class NativeModel:
             vals = list(cfg.get(k, []))[:5]
             getattr(c, k)[:len(vals)] = vals
         self.embed_dim = int(cfg['embed_dim'])
+        self.arch = arch
         self.device = device
         host = []
         ws = (spk_weight_t * len(state_dict))()
@@ -288,6 +289,12 @@ class NativeModel:
             lengths = torch.as_tensor(lengths, dtype=torch.int32).to(self.device).contiguous()
             if lengths.numel() != B:
                 raise HipError(f'lengths has {lengths.numel()} entries for a batch of {B}')
+            # a length past T would read the next utterance's rows (and past the workspace
+            # for the last one); CAM++'s unbiased std needs >= 2 frames
+            lo = 2 if self.arch == ARCH_CAMPPLUS else 1
+            mn, mx = (int(v) for v in torch.aminmax(lengths))
+            if mn < lo or mx > T:
+                raise HipError(f'lengths must lie in [{lo}, T={T}] (got min {mn}, max {mx})')
         with torch.cuda.device(self.device):
             need = self.workspace_bytes(B, T) if lengths is None else self.workspace_bytes_lengths(B, T, True)
             if self._ws is None or self._ws.numel() < need:

@@ -8,6 +8,7 @@ Same constructor and ``state_dict`` keys (231 tensors).  The forward is one nati
 Res2Net chain with the ``x_i + y_{i-1}`` add in the operand load, SE and attentive
 statistics pooling as reductions + small GEMMs.
 """
+import torch
 import torch.nn as nn
 
 from speakerlab import _hip
@@ -121,9 +122,25 @@ class ECAPA_TDNN(_hip.HipModuleMixin, nn.Module):
                     kernel_sizes=self.kernel_sizes, dilations=self.dilations)
 
     def forward(self, x, lengths=None):
-        """x: [B, T, input_size] on a ROCm device -> [B, lin_neurons].  ``lengths`` (relative
-        lengths for masked statistics) is not supported on the MI355X path: the reference
-        CLIs never pass it."""
-        if lengths is not None:
-            raise NotImplementedError('lengths masking is not implemented on the MI355X path')
-        return self._hip_forward(x)
+        """x: [B, T, input_size] on a ROCm device -> [B, lin_neurons].
+
+        ``lengths`` (reference semantics, ``ECAPA_TDNN.py:209-287, 430-454``): RELATIVE
+        lengths in (0, 1]; the convolutions still see the whole padded input and only the SE
+        squeeze means and the attentive-pooling statistics are masked to the frames
+        ``t < lengths[b] * T`` (``length_to_mask``).  The mask is evaluated here exactly as
+        the reference builds it (same dtype arithmetic), then passed to the kernels as
+        valid-frame counts."""
+        if lengths is None:
+            return self._hip_forward(x)
+        T = x.shape[1]
+        rel = torch.as_tensor(lengths)
+        if rel.dim() != 1 or rel.numel() != x.shape[0]:
+            raise ValueError(f'lengths must be 1-D with {x.shape[0]} entries')
+        if not rel.is_floating_point():
+            rel = rel.float()
+        rel = rel.detach().cpu()
+        frames = (torch.arange(T, dtype=rel.dtype).expand(len(rel), T) < (rel * T).unsqueeze(1)).sum(1)
+        if int(frames.min()) < 1:
+            raise ValueError('ECAPA lengths: every utterance needs at least one valid frame '
+                             '(the reference divides by the mask total)')
+        return self._hip_forward(x, lengths=frames.to(torch.int32))

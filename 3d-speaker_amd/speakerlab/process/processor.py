@@ -5,12 +5,41 @@
 [T, n_mels] computed by the HIP kernel (``csrc/fbank.hip``).  A device tensor stays on its
 device; a CPU tensor is moved to the current ROCm device for the computation and the
 result is returned on the CPU (same device-in/device-out contract as the reference).
-``FBank.batch`` is the batched form used by the CLIs (the reference vmaps ``__call__``,
-``infer_diarization.py:634``).
+
+The computation is the custom operator ``spk::fbank`` (``torch.library``) so that the
+reference's own batched call site, ``torch.vmap(self.feature_extractor)(wavs_batch)``
+(``infer_diarization.py:634``), works unchanged: the operator's vmap rule hands the whole
+[N, 1, L] batch to the batched kernel in one launch instead of looping.  ``FBank.batch``
+is the same batched form for callers that do not vmap.
 """
 import torch
 
 from speakerlab import _hip
+
+
+@torch.library.custom_op('spk::fbank', mutates_args=())
+def _fbank_op(wav: torch.Tensor, n_mels: int, mean_nor: bool) -> torch.Tensor:
+    """wav [1, L] (device) -> [T, n_mels]; the reference's per-call shape contract."""
+    return _hip.fbank(wav[0], n_mels, mean_nor)
+
+
+@_fbank_op.register_fake
+def _(wav, n_mels, mean_nor):
+    return wav.new_empty((_hip.num_frames(wav.shape[-1]), n_mels))
+
+
+def _fbank_vmap(info, in_dims, wav, n_mels, mean_nor):
+    """vmap rule: [N, 1, L] (batch dim anywhere) -> one batched kernel launch, [N, T, n_mels]."""
+    bdim = in_dims[0]
+    if bdim is None:
+        return _fbank_op(wav, n_mels, mean_nor), None
+    wav = wav.movedim(bdim, 0)
+    if wav.dim() != 3 or wav.shape[1] != 1:
+        raise _hip.HipError(f'FBank under vmap: expected per-sample [1, L], got {tuple(wav.shape[1:])}')
+    return _hip.fbank(wav[:, 0].contiguous(), n_mels, mean_nor), 0
+
+
+_fbank_op.register_vmap(_fbank_vmap)
 
 
 class FBank(object):
@@ -36,7 +65,7 @@ class FBank(object):
             wav = wav[0:1]
         assert wav.dim() == 2 and wav.shape[0] == 1
         dev_wav, back = self._on_device(wav)
-        feat = _hip.fbank(dev_wav[0], self.n_mels, self.mean_nor)
+        feat = _fbank_op(dev_wav.to(torch.float32), self.n_mels, bool(self.mean_nor))
         return feat if back is None else feat.to(back)
 
     def batch(self, wavs: torch.Tensor, lengths=None):

@@ -103,11 +103,16 @@ int spk_model_workspace_bytes(spk_model_t* model, int32_t B, int32_t T, size_t* 
 int spk_model_forward(spk_model_t* model, const float* feats, int32_t B, int32_t T, void* workspace,
                       size_t workspace_bytes, float* emb_out, void* stream);
 
-/* Variable-length batch (CAM++): feats is [B, T, feat_dim] with
- * utterance b occupying frames [0, lengths[b]) (lengths: DEVICE int32 [B], 2 <= lengths[b]
- * <= T; frames past it are ignored).  Every embedding equals the forward of that utterance
- * alone (no padding enters the computation).  lengths == NULL is spk_model_forward.
- * Replaces running the reference model (DTDNN.py:111-115) once per utterance.
+/* Variable-length batch: feats is [B, T, feat_dim] with utterance b occupying frames
+ * [0, lengths[b]) (lengths: DEVICE int32 [B]).  lengths == NULL is spk_model_forward.
+ *  - CAM++ (2 <= lengths[b] <= T): frames past lengths[b] are
+ *    ignored, every embedding equals the forward of that utterance alone (no padding
+ *    enters the computation).  Replaces running DTDNN.py:111-115 once per utterance.
+ *  - ECAPA-TDNN (1 <= lengths[b] <= T): the reference's forward(x, lengths)
+ *    (ECAPA_TDNN.py:209-287, 430-454): the convolutions run over the padded batch, the SE
+ *    squeeze means and the attentive-pooling statistics cover frames [0, lengths[b]) only.
+ *    (The reference takes RELATIVE lengths; the Python module converts them with the
+ *    reference's own mask arithmetic, length_to_mask :11-27.)
  * Other architectures return SPK_E_UNSUPPORTED for a non-NULL lengths. */
 int spk_model_workspace_bytes_lengths(spk_model_t* model, int32_t B, int32_t T, int32_t ragged, size_t* bytes);
 int spk_model_forward_lengths(spk_model_t* model, const float* feats, int32_t B, int32_t T, const int32_t* lengths,

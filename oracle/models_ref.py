@@ -151,8 +151,16 @@ def _tdnn_block(sd: SD, p: str, x, dilation=1):
     return _bn(F.relu(y), sd, p + '.norm.norm')
 
 
-def _seres2net_block(sd: SD, p: str, x, dilation, scale=8):
-    """SERes2NetBlock ECAPA_TDNN.py:290-347 with Res2NetBlock :154-191 and SEBlock :194-222."""
+def _length_mask(lengths, L):
+    """length_to_mask(lengths * L, max_len=L) ECAPA_TDNN.py:11-27, as [B, 1, L] in the dtype
+    of ``lengths`` (float32 for the reference's default ``torch.ones``), like the reference."""
+    m = torch.arange(L, dtype=lengths.dtype).expand(len(lengths), L) < (lengths * L).unsqueeze(1)
+    return m.to(lengths.dtype).unsqueeze(1)
+
+
+def _seres2net_block(sd: SD, p: str, x, dilation, scale=8, lengths=None):
+    """SERes2NetBlock ECAPA_TDNN.py:290-347 with Res2NetBlock :154-191 and SEBlock :194-222
+    (masked squeeze mean with relative ``lengths``, :209-216)."""
     residual = x
     if (p + '.shortcut.conv.weight') in sd:
         residual = _same_reflect_conv1d(x, sd[p + '.shortcut.conv.weight'], sd[p + '.shortcut.conv.bias'])
@@ -169,16 +177,24 @@ def _seres2net_block(sd: SD, p: str, x, dilation, scale=8):
         ys.append(y_i)
     x = torch.cat(ys, 1)
     x = _tdnn_block(sd, p + '.tdnn2', x)
-    s = x.mean(dim=2, keepdim=True)
+    if lengths is not None:
+        mask = _length_mask(lengths, x.shape[-1])
+        s = (x * mask).sum(dim=2, keepdim=True) / mask.sum(dim=2, keepdim=True)
+    else:
+        s = x.mean(dim=2, keepdim=True)
     s = F.relu(F.conv1d(s, sd[p + '.se_block.conv1.conv.weight'], sd[p + '.se_block.conv1.conv.bias']))
     s = torch.sigmoid(F.conv1d(s, sd[p + '.se_block.conv2.conv.weight'], sd[p + '.se_block.conv2.conv.bias']))
     return s * x + residual
 
 
-def _asp(sd: SD, p: str, x, eps=1e-12):
-    """AttentiveStatisticsPooling ECAPA_TDNN.py:243-287, global_context=True, lengths=None."""
+def _asp(sd: SD, p: str, x, eps=1e-12, lengths=None):
+    """AttentiveStatisticsPooling ECAPA_TDNN.py:243-287, global_context=True; relative
+    ``lengths`` mask the global statistics and the softmax (-inf fill)."""
     L = x.shape[-1]
-    m = torch.full((x.shape[0], 1, L), 1.0 / L, dtype=x.dtype)
+    if lengths is None:
+        lengths = torch.ones(x.shape[0])
+    mask = _length_mask(lengths, L)
+    m = mask / mask.sum(dim=2, keepdim=True).float()     # float32 weights, as the reference
 
     def stats(x, m):
         mean = (m * x).sum(2)
@@ -189,25 +205,27 @@ def _asp(sd: SD, p: str, x, eps=1e-12):
     attn = torch.cat([x, mean.unsqueeze(2).repeat(1, 1, L), std.unsqueeze(2).repeat(1, 1, L)], 1)
     attn = torch.tanh(_tdnn_block(sd, p + '.tdnn', attn))
     attn = F.conv1d(attn, sd[p + '.conv.conv.weight'], sd[p + '.conv.conv.bias'])
+    attn = attn.masked_fill(mask == 0, float('-inf'))
     attn = F.softmax(attn, dim=2)
     mean, std = stats(x, attn)
     return torch.cat((mean, std), 1).unsqueeze(2)
 
 
-def ecapa_forward(sd: SD, x, dilations=(1, 2, 3, 4, 1)):
-    """ECAPA_TDNN.forward ECAPA_TDNN.py:430-463. x: [B, T, F] -> [B, lin_neurons]."""
+def ecapa_forward(sd: SD, x, dilations=(1, 2, 3, 4, 1), lengths=None):
+    """ECAPA_TDNN.forward ECAPA_TDNN.py:430-463. x: [B, T, F] -> [B, lin_neurons];
+    ``lengths``: relative lengths (masked SE / ASP statistics)."""
     x = x.transpose(1, 2)
     xl = []
     x = _tdnn_block(sd, 'blocks.0', x, dilations[0])
     xl.append(x)
     i = 1
     while f'blocks.{i}.tdnn1.conv.conv.weight' in sd:
-        x = _seres2net_block(sd, f'blocks.{i}', x, dilations[i])
+        x = _seres2net_block(sd, f'blocks.{i}', x, dilations[i], lengths=lengths)
         xl.append(x)
         i += 1
     x = torch.cat(xl[1:], 1)
     x = _tdnn_block(sd, 'mfa', x)
-    x = _asp(sd, 'asp', x)
+    x = _asp(sd, 'asp', x, lengths=lengths)
     x = _bn(x, sd, 'asp_bn.norm')
     x = F.conv1d(x, sd['fc.conv.weight'], sd['fc.conv.bias'])
     return x.transpose(1, 2).squeeze(1)

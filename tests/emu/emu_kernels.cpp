@@ -227,37 +227,43 @@ int spk_symmetric_eig(float*, int64_t, int64_t, float*, void*) { return SPK_E_UN
 
 // ---- TDNN reductions (contracts of csrc/tdnn_ops.h)
 namespace spk {
-hipError_t launch_time_mean(const float* x, int B, int T, int C, int ld, float* out, int ldo, hipStream_t) {
+static int vframes(const int* vlen, int b, int T) { return vlen ? std::min(std::max(vlen[b], 1), T) : T; }
+hipError_t launch_time_mean(const float* x, int B, int T, int C, int ld, float* out, int ldo, hipStream_t,
+                            const int* vlen) {
   for (int b = 0; b < B; ++b)
     for (int c = 0; c < C; ++c) {
+      const int Tb = vframes(vlen, b, T);
       double s = 0;
-      for (int t = 0; t < T; ++t) s += x[((size_t)b * T + t) * ld + c];
-      out[(size_t)b * ldo + c] = (float)(s / T);
+      for (int t = 0; t < Tb; ++t) s += x[((size_t)b * T + t) * ld + c];
+      out[(size_t)b * ldo + c] = (float)(s / Tb);
     }
   return hipSuccess;
 }
-hipError_t launch_asp_stats(const float* x, int B, int T, int C, int ld, float eps, float* out, hipStream_t) {
+hipError_t launch_asp_stats(const float* x, int B, int T, int C, int ld, float eps, float* out, hipStream_t,
+                            const int* vlen) {
   for (int b = 0; b < B; ++b)
     for (int c = 0; c < C; ++c) {
+      const int Tb = vframes(vlen, b, T);
       double s = 0, q = 0;
-      for (int t = 0; t < T; ++t) s += x[((size_t)b * T + t) * ld + c];
-      const double mean = s / T;
-      for (int t = 0; t < T; ++t) { const double d = x[((size_t)b * T + t) * ld + c] - mean; q += d * d / T; }
+      for (int t = 0; t < Tb; ++t) s += x[((size_t)b * T + t) * ld + c];
+      const double mean = s / Tb;
+      for (int t = 0; t < Tb; ++t) { const double d = x[((size_t)b * T + t) * ld + c] - mean; q += d * d / Tb; }
       out[(size_t)b * 2 * C + c] = (float)mean;
       out[(size_t)b * 2 * C + C + c] = (float)std::sqrt(std::fmax(q, (double)eps));
     }
   return hipSuccess;
 }
 hipError_t launch_attn_pool(const float* l, int ldl, const float* x, int ldx, int B, int T, int C, float eps,
-                            float* out, hipStream_t) {
+                            float* out, hipStream_t, const int* vlen) {
   std::vector<double> p(T);
   for (int b = 0; b < B; ++b)
     for (int c = 0; c < C; ++c) {
+      const int Tb = vframes(vlen, b, T);
       double mx = -1e300, den = 0, mean = 0, q = 0;
-      for (int t = 0; t < T; ++t) mx = std::fmax(mx, l[((size_t)b * T + t) * ldl + c]);
-      for (int t = 0; t < T; ++t) { p[t] = std::exp(l[((size_t)b * T + t) * ldl + c] - mx); den += p[t]; }
-      for (int t = 0; t < T; ++t) mean += p[t] / den * x[((size_t)b * T + t) * ldx + c];
-      for (int t = 0; t < T; ++t) { const double d = x[((size_t)b * T + t) * ldx + c] - mean; q += p[t] / den * d * d; }
+      for (int t = 0; t < Tb; ++t) mx = std::fmax(mx, l[((size_t)b * T + t) * ldl + c]);
+      for (int t = 0; t < Tb; ++t) { p[t] = std::exp(l[((size_t)b * T + t) * ldl + c] - mx); den += p[t]; }
+      for (int t = 0; t < Tb; ++t) mean += p[t] / den * x[((size_t)b * T + t) * ldx + c];
+      for (int t = 0; t < Tb; ++t) { const double d = x[((size_t)b * T + t) * ldx + c] - mean; q += p[t] / den * d * d; }
       out[(size_t)b * 2 * C + c] = (float)mean;
       out[(size_t)b * 2 * C + C + c] = (float)std::sqrt(std::fmax(q, (double)eps));
     }

@@ -59,6 +59,17 @@ def test_processor_fbank_dropin():
     np.testing.assert_allclose(out_cpu_in.numpy(), out.cpu().numpy())
 
 
+def test_processor_fbank_under_vmap():
+    """The reference's diarization call site, unchanged: torch.vmap(FBank)(wavs[:, None, :])
+    (infer_diarization.py:634)."""
+    from speakerlab.process.processor import FBank
+    wavs = synthetic.pcm16_batch(6, 24000, seed=11)
+    fb = FBank(80, 16000, mean_nor=True)
+    out = torch.vmap(fb)(torch.from_numpy(wavs).cuda()[:, None, :])
+    assert out.shape == (6, fbank_ref.num_frames(24000), 80) and out.is_cuda
+    _check(out.cpu().numpy(), np.stack([fbank_ref.fbank(w, 80, True) for w in wavs]))
+
+
 def test_wav_to_embedding_end_to_end():
     wavs = synthetic.pcm16_batch(4, 32000, seed=77)
     m = helpers.loaded_module('eres2netv2')

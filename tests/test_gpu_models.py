@@ -121,3 +121,30 @@ def test_ragged_unsupported_arch_raises():
     x = torch.zeros(2, 98, 80, device='cuda')
     with pytest.raises(_hip.HipError):
         h.forward(x, lengths=torch.tensor([98, 50], dtype=torch.int32))
+
+
+def test_ecapa_forward_with_lengths_matches_reference():
+    """ECAPA_TDNN.forward(x, lengths) (ECAPA_TDNN.py:209-287, 430-454): relative lengths mask
+    the SE squeeze means and the attentive-pooling statistics; goldens from the reference
+    module (tests/golden/make_ecapa_lengths_golden.py)."""
+    import os
+    g = dict(np.load(os.path.join(helpers.GOLDEN, 'ecapa_lengths_golden.npz')))
+    m = gpu_module('ecapa')
+    with torch.no_grad():
+        emb = m(torch.from_numpy(g['feats']).cuda(), lengths=torch.from_numpy(g['lengths'])).cpu().numpy()
+        full = m(torch.from_numpy(g['feats']).cuda()).cpu().numpy()
+    e64 = helpers.rel_err(emb, g['emb64']).max()
+    e32 = helpers.rel_err(emb, g['emb32']).max()
+    print(f'ecapa lengths: rel err vs fp64 {e64:.2e}, vs fp32 {e32:.2e}')
+    assert e64 < TOL and e32 < TOL
+    # row 0 has relative length 1.0: identical to the unmasked forward
+    assert helpers.rel_err(emb[:1], full[:1]).max() < 1e-6
+
+
+@pytest.mark.parametrize('arch,lengths', [('campplus', [198, 199]), ('campplus', [1, 50]), ('ecapa', [0.0, 1.0])])
+def test_out_of_range_lengths_raise(arch, lengths):
+    """A length past T would read the next utterance (and past the workspace for the last
+    row); CAM++'s unbiased std needs >= 2 frames, ECAPA >= 1."""
+    x = torch.zeros(2, 198, 80, device='cuda')
+    with pytest.raises((_hip.HipError, ValueError)):
+        gpu_module(arch)(x, lengths=torch.tensor(lengths))
