@@ -14,7 +14,7 @@ rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
 if fatal $rc; then exit $rc; fi
 
 echo "== pytest -m gpu $(date +%T)"
-timeout -k 10 900 python -m pytest tests -m gpu -q -rf > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
 if fatal $rc; then exit $rc; fi
 

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 fatal() { case "$1" in 0|1) return 1;; *) return 0;; esac; }
 echo "== pytest -m gpu $(date +%T)"
-timeout -k 10 900 python -m pytest tests -m gpu -q -rf > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -8 gpurun_out/pytest_gpu.log
 if fatal $rc; then exit $rc; fi
 for a in eres2netv2 eres2net_large ecapa campplus; do
