@@ -52,23 +52,37 @@ def ahc_labels(S: np.ndarray, fix_cos_thr: float) -> np.ndarray:
     return fcluster(lin, -fix_cos_thr + adjust, criterion='distance') - 1
 
 
-def p_prune(A: np.ndarray, pval: float, min_pnum: int) -> np.ndarray:
-    """Zero the n_elems smallest entries of every row (cluster.py:64-77), vectorised."""
-    n = A.shape[0]
+def pruned_count(n: int, pval: float, min_pnum: int) -> int:
+    """Entries zeroed per row by ``p_pruning`` (cluster.py:67-73): the reference slices
+    ``argsort(row)[0:n_elems]`` with ``n_elems = min(int((1 - pval) * n), n - min_pnum)``, so a
+    negative n_elems (n < min_pnum) zeroes all but the |n_elems| largest entries, and a count
+    past n zeroes the whole row -- Python slice semantics, reproduced here."""
     n_elems = min(int((1 - pval) * n), n - min_pnum)
-    if n_elems > 0:
-        low = np.argsort(A, axis=1)[:, :n_elems]
+    return len(range(n)[0:n_elems])
+
+
+def p_prune(A: np.ndarray, pval: float, min_pnum: int) -> np.ndarray:
+    """Zero the smallest entries of every row (cluster.py:64-77), vectorised (stable sort:
+    ties go lowest index first, like the GPU kernel)."""
+    cnt = pruned_count(A.shape[0], pval, min_pnum)
+    if cnt > 0:
+        low = np.argsort(A, axis=1, kind='stable')[:, :cnt]
         np.put_along_axis(A, low, 0, axis=1)
     return A
+
+
+def laplacian(S: np.ndarray, pval: float, min_pnum: int) -> np.ndarray:
+    """p-pruning -> 0.5 (A + A^T) -> zero diagonal -> D - A (cluster.py:43-49, 64-84)."""
+    A = p_prune(np.array(S, copy=True), pval, min_pnum)
+    A = 0.5 * (A + A.T)
+    np.fill_diagonal(A, 0)
+    return np.diag(np.abs(A).sum(axis=1)) - A
 
 
 def spectral_labels(S: np.ndarray, min_num_spks=1, max_num_spks=10, pval=0.02, min_pnum=6, oracle_num=None):
     """Spectral clustering of a cosine affinity matrix (cluster.py:35-112)."""
     from sklearn.cluster._kmeans import k_means
-    A = p_prune(np.array(S, copy=True), pval, min_pnum)
-    A = 0.5 * (A + A.T)
-    np.fill_diagonal(A, 0)
-    L = np.diag(np.abs(A).sum(axis=1)) - A
+    L = laplacian(S, pval, min_pnum)
     lambdas, vecs = scipy.sparse.linalg.eigsh(L, k=min(max_num_spks + 1, L.shape[0]), which='SM')
     if oracle_num is not None:
         k = oracle_num
@@ -106,8 +120,7 @@ def spectral_labels_gpu(X, min_num_spks=1, max_num_spks=10, pval=0.02, min_pnum=
     t = torch.as_tensor(np.ascontiguousarray(X, dtype=np.float32)).cuda()
     n = t.shape[0]
     S = _hip.cosine_affinity(t)
-    n_elems = min(int((1 - pval) * n), n - min_pnum)
-    L = _hip.spectral_laplacian(S, n_elems)
+    L = _hip.spectral_laplacian(S, pruned_count(n, pval, min_pnum))
     del S
     kk = min(max_num_spks + 1, n)
     w, V = _hip.symmetric_eig(L)
