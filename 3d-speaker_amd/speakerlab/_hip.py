@@ -36,6 +36,16 @@ class spk_model_config_t(ctypes.Structure):
                 ('dilations', ctypes.c_int32 * 5), ('reserved', ctypes.c_int32 * 8)]
 
 
+SPK_CONSUME_TOPK = 1
+
+
+class spk_affinity_consumer_t(ctypes.Structure):
+    _fields_ = [('kind', ctypes.c_int32), ('k', ctypes.c_int32), ('exclude_self', ctypes.c_int32),
+                ('self_offset', ctypes.c_int64), ('threshold', ctypes.c_float), ('top_scores', ctypes.c_void_p),
+                ('top_index', ctypes.c_void_p), ('count_ge', ctypes.c_void_p), ('workspace', ctypes.c_void_p),
+                ('workspace_bytes', ctypes.c_size_t)]
+
+
 # every entry point of include/spk_hip.h: name -> (restype, argtypes)
 _P = ctypes.c_void_p
 SYMBOLS = {
@@ -67,6 +77,11 @@ SYMBOLS = {
     'spk_spectral_laplacian': (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, _P, ctypes.c_int64,
                                               _P, ctypes.c_size_t, _P]),
     'spk_symmetric_eig': (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int64, _P, _P]),
+    'spk_cosine_topk_workspace_bytes': (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64,
+                                                       ctypes.POINTER(ctypes.c_size_t)]),
+    'spk_cosine_topk': (ctypes.c_int, [_P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int32,
+                                       ctypes.POINTER(spk_affinity_consumer_t), _P]),
+    'spk_cosine_trials': (ctypes.c_int, [_P, _P, ctypes.c_int32, _P, _P, ctypes.c_int64, _P, _P]),
 }
 
 _lib = None
@@ -362,6 +377,53 @@ def cosine_affinity(a: torch.Tensor, b: Optional[torch.Tensor] = None, out: Opti
     with torch.cuda.device(a.device):
         _check(lib().spk_cosine_affinity(a.data_ptr(), a.shape[0], b.data_ptr(), b.shape[0], a.shape[1],
                                          out.data_ptr(), out.stride(0), _stream(a.device)), 'spk_cosine_affinity')
+    return out
+
+
+def cosine_topk(a: torch.Tensor, b: torch.Tensor, k: int = 1, self_offset: Optional[int] = None,
+                threshold: float = float('inf')):
+    """Row-block consumer of the cosine affinity (the [Na, Nb] matrix is never written): for
+    every row of ``a`` the ``k`` best (score, column) pairs over ``b`` -- score descending,
+    column ascending on ties, column ``i + self_offset`` of row ``i`` excluded when
+    ``self_offset`` is given -- and the number of columns scoring >= ``threshold``.
+    Returns (scores [Na, k] float32, index [Na, k] int64, count [Na] int64)."""
+    require_device_tensor(a, 'cosine_topk')
+    b = a if b is None else b
+    a = a.to(torch.float32).contiguous()
+    b = b.to(torch.float32).contiguous()
+    if not 1 <= k <= 8:
+        raise HipError('cosine_topk: k must be in 1..8')
+    Na, Nb, E = a.shape[0], b.shape[0], a.shape[1]
+    dev = a.device
+    scores = torch.empty((Na, k), dtype=torch.float32, device=dev)
+    index = torch.empty((Na, k), dtype=torch.int64, device=dev)
+    count = torch.empty(Na, dtype=torch.int64, device=dev)
+    nbytes = ctypes.c_size_t(0)
+    _check(lib().spk_cosine_topk_workspace_bytes(Na, Nb, ctypes.byref(nbytes)), 'spk_cosine_topk_workspace_bytes')
+    ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=dev)
+    c = spk_affinity_consumer_t(SPK_CONSUME_TOPK, k, 0 if self_offset is None else 1,
+                                0 if self_offset is None else int(self_offset), float(threshold), scores.data_ptr(),
+                                index.data_ptr(), count.data_ptr(), ws.data_ptr(), nbytes.value)
+    with torch.cuda.device(dev):
+        _check(lib().spk_cosine_topk(a.data_ptr(), Na, b.data_ptr(), Nb, E, ctypes.byref(c), _stream(dev)),
+               'spk_cosine_topk')
+    return scores, index, count
+
+
+def cosine_trials(a: torch.Tensor, b: torch.Tensor, ia: torch.Tensor, ib: torch.Tensor) -> torch.Tensor:
+    """scores[t] = cosine(a[ia[t]], b[ib[t]]) on the device (compute_score_metrics.py:102-118)."""
+    require_device_tensor(a, 'cosine_trials')
+    a = a.to(torch.float32).contiguous()
+    b = b.to(torch.float32).contiguous()
+    ia = ia.to(device=a.device, dtype=torch.int64).contiguous()
+    ib = ib.to(device=a.device, dtype=torch.int64).contiguous()
+    if ia.numel() and (int(ia.min()) < 0 or int(ia.max()) >= a.shape[0] or int(ib.min()) < 0
+                       or int(ib.max()) >= b.shape[0]):
+        raise HipError('cosine_trials: trial index out of range')
+    out = torch.empty(ia.numel(), dtype=torch.float32, device=a.device)
+    with torch.cuda.device(a.device):
+        _check(lib().spk_cosine_trials(a.data_ptr(), b.data_ptr(), a.shape[1], ia.data_ptr(), ib.data_ptr(),
+                                       ia.numel(), out.data_ptr(), _stream(a.device)), 'spk_cosine_trials')
     return out
 
 

@@ -36,7 +36,6 @@ parser.add_argument('--c_fa', default=1, type=float, help='c_fa in DCF')
 parser.add_argument('--no_plot', action='store_true', help='MI355X build: skip the EER curve PNG')
 
 LABELS = {'1': 1, 'target': 1, '0': 0, 'nontarget': 0}
-ROW_BLOCK_ENTRIES = 1 << 27            # 512 MB of fp32 affinity per block
 
 
 def collect(data_dir):
@@ -66,7 +65,8 @@ def parse_trials(path):
 
 
 def trial_scores(enrol, test, pairs, device='cuda'):
-    """Cosine score of every (enrol, test) trial from row blocks of the GPU affinity."""
+    """Cosine score of every (enrol, test) trial, gathered on the GPU (``spk_cosine_trials``:
+    one wave per trial, O(trials x E) instead of the enrol x test affinity)."""
     from speakerlab import _hip
     ekeys = sorted({p[0] for p in pairs})
     tkeys = sorted({p[1] for p in pairs})
@@ -74,16 +74,9 @@ def trial_scores(enrol, test, pairs, device='cuda'):
     tidx = {k: i for i, k in enumerate(tkeys)}
     ea = torch.from_numpy(np.stack([np.asarray(enrol[k], np.float32).reshape(-1) for k in ekeys])).to(device)
     tb = torch.from_numpy(np.stack([np.asarray(test[k], np.float32).reshape(-1) for k in tkeys])).to(device)
-    rows = torch.tensor([eidx[p[0]] for p in pairs], dtype=torch.int64, device=device)
-    cols = torch.tensor([tidx[p[1]] for p in pairs], dtype=torch.int64, device=device)
-    scores = torch.empty(len(pairs), dtype=torch.float32, device=device)
-    block = max(1, ROW_BLOCK_ENTRIES // max(1, len(tkeys)))
-    for r0 in range(0, len(ekeys), block):
-        r1 = min(len(ekeys), r0 + block)
-        aff = _hip.cosine_affinity(ea[r0:r1], tb)
-        sel = (rows >= r0) & (rows < r1)
-        scores[sel] = aff[rows[sel] - r0, cols[sel]]
-    return scores.cpu().numpy()
+    rows = torch.tensor([eidx[p[0]] for p in pairs], dtype=torch.int64)
+    cols = torch.tensor([tidx[p[1]] for p in pairs], dtype=torch.int64)
+    return _hip.cosine_trials(ea, tb, rows, cols).cpu().numpy()
 
 
 def plot_eer_curves(fnr, fpr, scores, thres, labels, save_path):

@@ -52,3 +52,13 @@ def affinity_row_block(emb_all: torch.Tensor, rank: int, world: int, out: Option
     from speakerlab import _hip
     s, e = shard_bounds(emb_all.shape[0], rank, world)
     return s, _hip.cosine_affinity(emb_all[s:e], emb_all, out=out)
+
+
+def topk_row_block(emb_all: torch.Tensor, rank: int, world: int, k: int = 1, threshold: float = float('inf')):
+    """This rank's row block consumed in place: for each of its rows the k best matches among
+    all N embeddings (self excluded) and the count of scores >= threshold (``spk_cosine_topk``;
+    the row block of the affinity is never written).  Returns (row0, scores, index, count)."""
+    from speakerlab import _hip
+    s, e = shard_bounds(emb_all.shape[0], rank, world)
+    sc, ix, cnt = _hip.cosine_topk(emb_all[s:e], emb_all, k=k, self_offset=s, threshold=threshold)
+    return s, sc, ix, cnt

@@ -23,6 +23,9 @@
  *                        OnnxSpeakerEmbeddingModel::extract_embedding speaker_embedding_model.cpp:42-69)
  *   spk_cosine_affinity  sklearn cosine_similarity as used by speakerlab/process/cluster.py:59-62,150
  *                        and speakerlab/bin/compute_score_metrics.py:110-114
+ *   spk_cosine_topk      the consumers of the row-block affinity: best matches
+ *                        per row / threshold counts, the affinity never materialised
+ *   spk_cosine_trials    the per-trial cosine_similarity loop of compute_score_metrics.py:102-118
  */
 #ifndef SPK_HIP_H
 #define SPK_HIP_H
@@ -140,6 +143,35 @@ int spk_model_forward_timed(spk_model_t* model, const float* feats, int32_t B, i
  * zero-norm rows left as zero). */
 int spk_cosine_affinity(const float* Ea, int64_t Na, const float* Eb, int64_t Nb, int32_t E, float* out,
                         int64_t ldo, void* stream);
+
+/* Consumers of the cosine affinity, applied where each tile is produced (the N x Nb matrix is
+ * never written): for every row i of Ea, the k best (score, column) pairs over Eb, ordered by
+ * score descending then column ascending, and the number of columns with score >= threshold.
+ * exclude_self drops column i + self_offset of row i (a rank's row block [r0, r1) of the
+ * all-gathered embeddings: self_offset = r0).  Outputs (device, any may be NULL):
+ * top_scores [Na][k] float32, top_index [Na][k] int64 (-1 when fewer than k columns),
+ * count_ge [Na] int64.  workspace: device, spk_cosine_topk_workspace_bytes(Na, Nb). */
+#define SPK_CONSUME_TOPK 1
+typedef struct {
+  int32_t kind;            /* SPK_CONSUME_TOPK */
+  int32_t k;               /* 1..8 */
+  int32_t exclude_self;
+  int64_t self_offset;
+  float threshold;
+  float* top_scores;
+  int64_t* top_index;
+  int64_t* count_ge;
+  void* workspace;
+  size_t workspace_bytes;
+} spk_affinity_consumer_t;
+int spk_cosine_topk_workspace_bytes(int64_t Na, int64_t Nb, size_t* bytes);
+int spk_cosine_topk(const float* Ea, int64_t Na, const float* Eb, int64_t Nb, int32_t E,
+                    const spk_affinity_consumer_t* consumer, void* stream);
+
+/* Trial scoring: scores[t] = cosine(Ea[ia[t]], Eb[ib[t]]) for n_trials (enrol, test) index
+ * pairs (device int64 arrays), sklearn semantics (zero-norm rows divide by 1). */
+int spk_cosine_trials(const float* Ea, const float* Eb, int32_t E, const int64_t* ia, const int64_t* ib,
+                      int64_t n_trials, float* scores, void* stream);
 
 /* Spectral clustering preparation (reference cluster.py SpectralCluster.p_pruning :64-77
  * and get_laplacian :79-84): S is the N x N cosine affinity (row stride lds); every row's

@@ -2,7 +2,7 @@
 rocSOLVER eigenpairs) vs fixtures produced by the REFERENCE ``speakerlab/process/cluster.py``
 (``tests/golden/make_cluster_golden.py``).  The GPU affinity differs from sklearn's float32
 GEMM in the last bits, so labels are compared as partitions (cluster ids relabelled by first
-occurrence) and the Laplacian to 2e-6; the host decisions on identical affinities are pinned
+occurrence) and the Laplacian to 2e-6 + 1e-6 relative (the degree diagonal); the host decisions on identical affinities are pinned
 bit for bit by ``tests/test_cluster_golden.py``."""
 import json
 import os
@@ -45,7 +45,7 @@ def test_gpu_laplacian_matches_reference(key):
     S = _hip.cosine_affinity(torch.from_numpy(X).cuda())
     Lg = _hip.spectral_laplacian(S, C.pruned_count(n, float(p[1:]), int(m[1:]))).cpu().numpy()
     np.testing.assert_array_equal(Lg == 0, L == 0)          # the same entries pruned
-    np.testing.assert_allclose(Lg, L, rtol=0, atol=2e-6)
+    np.testing.assert_allclose(Lg, L, rtol=1e-6, atol=2e-6)
     if f'{key}/lambdas' in G.files:
         w, _ = _hip.symmetric_eig(torch.from_numpy(L.copy()).cuda())
         lam = w.cpu().numpy()[:11]

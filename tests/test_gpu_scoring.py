@@ -34,7 +34,6 @@ def test_score_metrics_cli(tmp_path, monkeypatch):
                 nb = np.linalg.norm(b)
                 ref.append(0.0 if nb == 0 else a @ b / (np.linalg.norm(a) * nb))
     (tmp_path / 'trials').write_text('\n'.join(lines) + '\n')
-    monkeypatch.setattr(csm, 'ROW_BLOCK_ENTRIES', 7 * 60)    # several row blocks
     res = csm.main(['--enrol_data', str(tmp_path / 'enrol'), '--test_data', str(tmp_path / 'test'),
                     '--scores_dir', str(tmp_path / 'scores'), '--trials', str(tmp_path / 'trials')])
     got = np.array([float(l.split()[-1]) for l in (tmp_path / 'scores' / 'trials.score').read_text().splitlines()])

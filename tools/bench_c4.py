@@ -84,18 +84,10 @@ def main():
                 emb_local[a:b] = model(feats)
 
     def score(emb_all):
-        # top-1 trial score of every row of this rank's block against all N (self excluded)
-        best = torch.empty(n_local, dtype=torch.float32, device=device)
-        arg = torch.empty(n_local, dtype=torch.int64, device=device)
-        chunk = torch.empty((args.chunk_rows, emb_all.shape[0]), dtype=torch.float32, device=device)
-        for a in range(0, n_local, args.chunk_rows):
-            b = min(n_local, a + args.chunk_rows)
-            c = chunk[:b - a]
-            _hip.cosine_affinity(emb_all[s0 + a:s0 + b], emb_all, out=c)
-            r = torch.arange(b - a, device=device)
-            c[r, s0 + a + r] = -2.0
-            best[a:b], arg[a:b] = c.max(dim=1)
-        return best, arg
+        # top-1 trial score of every row of this rank's block against all N (self excluded),
+        # reduced inside the affinity kernel (spk_cosine_topk): no N_local x N matrix is written
+        sc, ix, _ = _hip.cosine_topk(emb_all[s0:s1], emb_all, k=1, self_offset=s0)
+        return sc[:, 0], ix[:, 0]
 
     def gather():
         if world > 1:
@@ -108,7 +100,7 @@ def main():
             model(_hip.fbank(wav[:args.batch], 80, mean_nor=True))
         if world > 1:
             all_gather_embeddings(emb_local[:min(n_local, 8)], min(args.utts, 8 * world))
-        _hip.cosine_affinity(emb_local[:256], emb_local[:1024])
+        _hip.cosine_topk(emb_local[:256], emb_local[:1024], k=1, self_offset=0)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
