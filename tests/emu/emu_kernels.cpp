@@ -169,6 +169,17 @@ hipError_t launch_fbank(const float*, const int64_t*, int, float*, const int64_t
   return hipErrorNotSupported;
 }
 
+// affinity consumers (affinity.hip): GPU-only, not part of any launch plan
+size_t cosine_topk_workspace(long long, long long) { return 0; }
+hipError_t launch_cosine_topk(const float*, long long, const float*, long long, int, int, long long, int, float, void*,
+                              size_t, float*, long long*, long long*, hipStream_t) {
+  return hipErrorNotSupported;
+}
+hipError_t launch_cosine_trials(const float*, const float*, int, const long long*, const long long*, long long, float*,
+                                hipStream_t) {
+  return hipErrorNotSupported;
+}
+
 hipError_t launch_cosine_affinity(const float* A, long long Na, const float* B, long long Nb, int E, float* out,
                                   long long ldo, hipStream_t) {
   for (long long i = 0; i < Na; ++i)
