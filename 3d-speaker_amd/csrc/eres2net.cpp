@@ -17,9 +17,11 @@
 //   * `sp + spx` is fused into the 3x3 conv's operand load; AFF is two GEMMs, the second
 //     applying x*(1+tanh a) + y*(1-tanh a) in its epilogue.
 #include <cmath>
+#include <cstdlib>
 
 #include "aff.h"
 #include "misc.h"
+#include "res2block.h"
 #include "runtime.h"
 
 namespace spk {
@@ -130,9 +132,49 @@ struct ERes2Builder {
     b.conv(p + ".local_att.3", e, a1, io2);
   }
 
+  // The whole block as one fused kernel (res2block.hip): ERes2NetV2 stage-1 shape (scale 2,
+  // identity shortcut, 128 channels, slices <= 32 wide), fp16x3 path, uniform lengths.
+  bool fusable(const std::string& p, const T4& x, int stride, int width, int Cout, bool use_aff) const {
+    return v2 && !use_aff && stride == 1 && scale == 2 && width <= 32 && x.C == 128 && Cout == 128 &&
+           x.ld == x.C && !m.has(p + ".shortcut.0.weight") && !b.ragged && conv_use_x3() &&
+           std::getenv("SPK_NO_BLOCK_FUSION") == nullptr;
+  }
+
+  T4 fused_block(const std::string& p, const T4& x, int width, Buf outbuf) {
+    const ChanMap xin = ChanMap::dense(x.C);
+    const ChanMap sl = ChanMap::slices(width, 2, 32);
+    const ChanMap w32 = ChanMap::dense(width, 32);
+    const Packed& c1 = m.pack(p + ".conv1#fused", sl, {Part{p + ".conv1.weight", "", p + ".bn1", xin, 0, 0}}, x.C);
+    const Packed& ca = m.pack(p + ".convs.0#fused", w32, {Part{p + ".convs.0.weight", "", p + ".bns.0", w32, 0, 0}}, 9 * 32);
+    const Packed& cb = m.pack(p + ".convs.1#fused", w32, {Part{p + ".convs.1.weight", "", p + ".bns.1", w32, 0, 0}}, 9 * 32);
+    const Packed& c3 = m.pack(p + ".conv3#fused", xin, {Part{p + ".conv3.weight", "", p + ".bn3", sl, 0, 0}}, 64);
+    const double px = (double)x.H * x.W;
+    b.macs_per_utt += px * x.C * (double)width * 2 + 2.0 * px * 9.0 * width * width + px * (double)width * 2 * x.C;
+    T4 out{outbuf, x.C, x.H, x.W, x.C};
+    if (b.plan) {
+      Res2Desc d;
+      d.nimg = b.B; d.H = x.H; d.W = x.W; d.C = x.C; d.width = width;
+      d.w1h = m.dhi(c1.w_off); d.w1l = m.dlo(c1.w_off); d.b1 = m.dptr(c1.b_off);
+      d.wah = m.dhi(ca.w_off); d.wal = m.dlo(ca.w_off); d.ba = m.dptr(ca.b_off);
+      d.wbh = m.dhi(cb.w_off); d.wbl = m.dlo(cb.w_off); d.bb = m.dptr(cb.b_off);
+      d.w3h = m.dhi(c3.w_off); d.w3l = m.dlo(c3.w_off); d.b3 = m.dptr(c3.b_off);
+      d.w1 = m.dptr(c1.w_off); d.wa = m.dptr(ca.w_off); d.wb = m.dptr(cb.w_off); d.w3 = m.dptr(c3.w_off);
+      const double bytes = 8.0 * b.B * px * x.C +
+                           4.0 * ((double)c1.N * c1.K + (double)ca.N * ca.K + (double)cb.N * cb.K + (double)c3.N * c3.K);
+      const Buf xb = x.buf, ob = outbuf;
+      b.step(p + ".fused", [d, xb, ob](const Ctx& c) mutable {
+        d.x = c.resolve(xb);
+        d.out = c.resolve(ob);
+        return launch_res2_block(d, c.stream);
+      }, res2_block_kernel_name(d), bytes);
+    }
+    return out;
+  }
+
   T4 block(const std::string& p, const T4& x, int stride, int width, int planes, bool use_aff, Buf outbuf) {
     const int Ho = (x.H - 1) / stride + 1, Wo = (x.W - 1) / stride + 1;
     const int Cout = planes * expansion;
+    if (fusable(p, x, stride, width, Cout, use_aff)) return fused_block(p, x, width, outbuf);
     const ChanMap sl = ChanMap::slices(width, scale);
     const int wp = sl.n_phys / scale;
     const int ldt = sl.n_phys;

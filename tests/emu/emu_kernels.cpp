@@ -19,6 +19,7 @@
 #include "../../3d-speaker_amd/csrc/fbank.h"
 #include "../../3d-speaker_amd/csrc/misc.h"
 #include "../../3d-speaker_amd/csrc/aff.h"
+#include "../../3d-speaker_amd/csrc/res2block.h"
 
 namespace spk {
 
@@ -167,6 +168,64 @@ hipError_t launch_tstp(const float* x, int B, int H, int W, int C, int ld, float
 hipError_t launch_fbank(const float*, const int64_t*, int, float*, const int64_t*, int, int, const FbankTables*,
                         hipStream_t, int) {
   return hipErrorNotSupported;
+}
+
+bool conv_use_x3() {
+  const char* e = std::getenv("SPK_CONV_MFMA");
+  return !(e && std::string(e) == "f32");
+}
+
+// fused Res2Net block (res2block.hip), the kernel's contract in double precision:
+// conv1 + bn1 + Hardtanh -> s0 | s1 (32-channel slices), y0 = Ht(conv3x3(s0)),
+// y1 = Ht(conv3x3(y0 + s1)), out = Ht(conv3(cat(y0, y1)) + x), zero padding at the edges
+bool res2_block_supported(const Res2Desc& d) {
+  return d.C == 128 && d.width >= 1 && d.width <= 32 && d.w1 && d.wa && d.wb && d.w3 && d.b1 && d.ba && d.bb && d.b3;
+}
+std::string res2_block_kernel_name(const Res2Desc& d) { return "emu_res2_block<" + std::to_string(d.C) + ">"; }
+hipError_t launch_res2_block(const Res2Desc& d, hipStream_t) {
+  if (!res2_block_supported(d) || d.x == d.out) return hipErrorInvalidValue;
+  const int H = d.H, W = d.W, C = d.C;
+  auto ht = [](double v) { return std::min(std::max(v, 0.0), 20.0); };
+  std::vector<double> t1((size_t)H * W * 64), y0((size_t)H * W * 32), sp((size_t)H * W * 32), y1((size_t)H * W * 32);
+  auto conv3 = [&](const std::vector<double>& in, const float* w, const float* b, std::vector<double>& out) {
+    for (int y = 0; y < H; ++y)
+      for (int x = 0; x < W; ++x)
+        for (int n = 0; n < 32; ++n) {
+          double acc = b[n];
+          for (int tap = 0; tap < 9; ++tap) {
+            const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+            if (yy < 0 || yy >= H || xx < 0 || xx >= W) continue;
+            const double* iv = &in[((size_t)yy * W + xx) * 32];
+            for (int c = 0; c < 32; ++c) acc += (double)w[(size_t)n * 288 + tap * 32 + c] * iv[c];
+          }
+          out[((size_t)y * W + x) * 32 + n] = ht(acc);
+        }
+  };
+  for (int img = 0; img < d.nimg; ++img) {
+    const float* xi = d.x + (size_t)img * H * W * C;
+    float* oi = d.out + (size_t)img * H * W * C;
+    for (size_t p = 0; p < (size_t)H * W; ++p)
+      for (int n = 0; n < 64; ++n) {
+        double acc = d.b1[n];
+        for (int k = 0; k < C; ++k) acc += (double)d.w1[(size_t)n * C + k] * xi[p * C + k];
+        t1[p * 64 + n] = ht(acc);
+      }
+    std::vector<double> s0((size_t)H * W * 32);
+    for (size_t p = 0; p < (size_t)H * W; ++p)
+      for (int c = 0; c < 32; ++c) s0[p * 32 + c] = t1[p * 64 + c];
+    conv3(s0, d.wa, d.ba, y0);
+    for (size_t p = 0; p < (size_t)H * W; ++p)
+      for (int c = 0; c < 32; ++c) sp[p * 32 + c] = y0[p * 32 + c] + t1[p * 64 + 32 + c];
+    conv3(sp, d.wb, d.bb, y1);
+    for (size_t p = 0; p < (size_t)H * W; ++p)
+      for (int n = 0; n < C; ++n) {
+        double acc = d.b3[n] + xi[p * C + n];
+        for (int c = 0; c < 32; ++c)
+          acc += (double)d.w3[(size_t)n * 64 + c] * y0[p * 32 + c] + (double)d.w3[(size_t)n * 64 + 32 + c] * y1[p * 32 + c];
+        oi[p * C + n] = (float)ht(acc);
+      }
+  }
+  return hipSuccess;
 }
 
 // affinity consumers (affinity.hip): GPU-only, not part of any launch plan
