@@ -20,6 +20,7 @@ struct AffDesc {
   // local_att.3 (+ local_att.4 BN folded): [cp][kp2] over K = nmid, bias [cp]
   const float* w2 = nullptr; const uint16_t* w2h = nullptr; const uint16_t* w2l = nullptr;
   const float* b2 = nullptr; int kp2 = 0;
+  int* range_flag = nullptr;                  // fp16x3 range guard (common.h)
 };
 
 // true when launch_aff_x3 serves this geometry (fp16x3 path on, nmid 32 / 64, cp % 8 == 0)

@@ -61,6 +61,7 @@ __global__ void __launch_bounds__(256) aff_x3_kernel(const AffDesc a) {
   const float* yr = a.y + (size_t)m * a.ldy;
   const int K = 2 * a.cp;
 
+  float amax = 0.f;                                 // range guard (common.h) on the outputs
   // ---- stage 1
   f32x16 h[MT], hx[MT];
 #pragma unroll
@@ -173,12 +174,16 @@ __global__ void __launch_bounds__(256) aff_x3_kernel(const AffDesc a) {
         const float sg = __frcp_rn(1.0f + __expf(-2.0f * (zq[e] + bias[e])));
         o[e] = 2.0f * fmaf(sg, xv[q][e] - yv[q][e], yv[q][e]);
       }
-      if (m0 + p < a.M && n0 + c4 < a.cp) *reinterpret_cast<f32x4*>(a.out + (size_t)(m0 + p) * a.ldo + n0 + c4) = o;
+      if (m0 + p < a.M && n0 + c4 < a.cp) {
+        amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+        *reinterpret_cast<f32x4*>(a.out + (size_t)(m0 + p) * a.ldo + n0 + c4) = o;
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // slab reads done before the next chunk
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  range_note(a.range_flag, amax);
 }
 
 }  // namespace

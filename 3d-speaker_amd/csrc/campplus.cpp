@@ -59,9 +59,10 @@ void build_campplus(Builder& b, int T) {
     const int kp = stem.Kp;
     const Buf xo = x.buf;
     const bool rg = b.ragged;
+    int* flag = b.exact ? nullptr : m.range_flag;
     b.step("head.stem", [=](const Ctx& c) {
       return launch_stem_conv3x3(c.in, B, T, F, w, bias, mc, ACT_RELU, kp, c.resolve(xo), mc, c.stream,
-                                 rg ? c.lens : nullptr);
+                                 rg ? c.lens : nullptr, flag);
     });
   }
   const ChanMap cm = ChanMap::dense(mc);

@@ -65,7 +65,23 @@ struct ConvDesc {
   int gate_nseg = 0;
   int ksplit = 1; float* partial = nullptr;            // split-K partial slabs [ksplit][M][N]
   const int* rowlen = nullptr;  // ragged batches: outputs with wo >= rowlen[img] are written as 0
+  int* range_flag = nullptr;    // fp16x3 range guard (below): set when an output reaches kRangeLimit
 };
+
+// fp16x3 range guard.  The split-precision GEMMs represent an operand as two fp16 values,
+// so an activation at or above fp16's largest finite value (65504) would saturate silently.
+// Every producer of an unbounded activation that a split GEMM later reads (conv / linear
+// epilogues, the ERes2Net stem, AFF, the model input) ORs 1 into the handle's flag word when
+// any output it writes reaches 2^15; the ops between two GEMMs grow a value at most 2x
+// (AFF combine, residual + Hardtanh), so below the limit nothing can saturate.  The host
+// reads the flag after the forward and re-runs it on the exact-fp32 kernels when it is set
+// (spk_model_range_check / spk_model_forward_exact).
+constexpr float kRangeLimit = 32768.0f;
+#ifdef __HIPCC__
+__device__ __forceinline__ void range_note(int* flag, float amax) {
+  if (flag && amax >= kRangeLimit) atomicOr(flag, 1);
+}
+#endif
 
 // XCD-aware bijective block remap: consecutive logical ids (same M tile, all N tiles) are
 // placed on one XCD so the A tile they share stays in that XCD's L2 (the dispatcher deals

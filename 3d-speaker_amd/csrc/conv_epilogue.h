@@ -97,6 +97,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
   // Common case (bias / residual / activations / post-affine only): every residual load of
   // the wave is issued before the first use, so the whole epilogue is one memory round trip.
   constexpr int NTL = TM * TN;
+  float amax = 0.f;                            // range guard (common.h)
   if constexpr (NTL <= 2) {
     if (LEAN || (vec && !part && !d.affx && !d.gate && !d.rowbias)) {
       const int c4 = (lane & 7) * 4;
@@ -141,9 +142,11 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
             o[e] = apply_act(x, d.act2);
           }
           if (row_masked(d, m)) o = f32x4{0.f, 0.f, 0.f, 0.f};
+          amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
           *reinterpret_cast<f32x4*>(ocol + (size_t)m * d.ldo) = o;
         }
       }
+      range_note(d.range_flag, amax);
       return;
     }
     // AFF second conv (fusion.py:26-28): x*(1+tanh v) + y*(1-tanh v) replaces the
@@ -187,9 +190,11 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
             o[e] = xa[tile][q][e] * t + ya[tile][q][e] * (2.0f - t);
           }
           if (row_masked(d, m)) o = f32x4{0.f, 0.f, 0.f, 0.f};
+          amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
           *reinterpret_cast<f32x4*>(ocol + (size_t)m * d.ldo) = o;
         }
       }
+      range_note(d.range_flag, amax);
       return;
     }
   }
@@ -260,6 +265,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
               }
             }
             if (row_masked(d, m)) o = f32x4{0.f, 0.f, 0.f, 0.f};
+            amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
             *reinterpret_cast<f32x4*>(ocol + (size_t)m * d.ldo) = o;
           }
         }
@@ -272,13 +278,19 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
           const int m = rowmap(i * 32 + rl);
           if (m >= 0 && m < M && n < d.N) {
             const float v = ct[rl * 32 + li];
-            if (part) part[(size_t)m * d.N + n] = v;
-            else ocol[(size_t)m * d.ldo] = epilogue_elem(d, m, n, v);
+            if (part) {
+              part[(size_t)m * d.N + n] = v;
+            } else {
+              const float o = epilogue_elem(d, m, n, v);
+              amax = fmaxf(amax, fabsf(o));
+              ocol[(size_t)m * d.ldo] = o;
+            }
           }
         }
       }
     }
   }
+  range_note(d.range_flag, amax);
 }
 
 }  // namespace spk

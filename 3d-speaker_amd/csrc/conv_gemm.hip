@@ -343,12 +343,16 @@ conv_gemm_x3_kernel(const ConvDesc d) {
 // Split-K combine: out = epi(sum_z partial[z])   (fixed z order: deterministic)
 __global__ void splitk_reduce_kernel(const ConvDesc d, int M) {
   const size_t total = (size_t)M * d.N;
+  float amax = 0.f;
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
     const int m = e / d.N, n = e % d.N;
     float v = 0.f;
     for (int z = 0; z < d.ksplit; ++z) v += d.partial[(size_t)z * total + e];
-    *out_at(d, m, n) = epilogue_elem(d, m, n, v);
+    const float o = epilogue_elem(d, m, n, v);
+    amax = fmaxf(amax, fabsf(o));
+    *out_at(d, m, n) = o;
   }
+  range_note(d.range_flag, amax);
 }
 
 // fp16x3 split-precision MFMA (default) or exact fp32 MFMA (SPK_CONV_MFMA=f32)

@@ -89,7 +89,7 @@ struct ERes2Builder {
       b.macs_per_utt += m0 + m3;
       return;
     }
-    if (aff_x3_supported(cp, mid.n_phys)) {
+    if (b.x3() && aff_x3_supported(cp, mid.n_phys)) {
       // one fused kernel (aff.hip): x and y read once, h never leaves registers
       b.macs_per_utt += m0 + m3;
       AffDesc ad;
@@ -100,6 +100,7 @@ struct ERes2Builder {
       ad.b1 = m.dptr(a0.b_off); ad.kp1 = a0.Kp;
       ad.w2 = m.dptr(a1.w_off); ad.w2h = m.dhi(a1.w_off); ad.w2l = m.dlo(a1.w_off);
       ad.b2 = m.dptr(a1.b_off); ad.kp2 = a1.Kp;
+      ad.range_flag = m.range_flag;
       if (!a0.has_bias || !a1.has_bias) throw SpkError(SPK_E_WEIGHTS, p + ": AFF convs without bias");
       const double bytes = 4.0 * ad.M * (3.0 * C) + 4.0 * ((double)a0.N * a0.K + (double)a1.N * a1.K);
       const Buf xb = x.buf, yb = y.buf, ob = out.buf;
@@ -136,7 +137,7 @@ struct ERes2Builder {
   // identity shortcut, 128 channels, slices <= 32 wide), fp16x3 path, uniform lengths.
   bool fusable(const std::string& p, const T4& x, int stride, int width, int Cout, bool use_aff) const {
     return v2 && !use_aff && stride == 1 && scale == 2 && width <= 32 && x.C == 128 && Cout == 128 &&
-           x.ld == x.C && !m.has(p + ".shortcut.0.weight") && !b.ragged && conv_use_x3() &&
+           x.ld == x.C && !m.has(p + ".shortcut.0.weight") && !b.ragged && b.x3() &&
            std::getenv("SPK_NO_BLOCK_FUSION") == nullptr;
   }
 
@@ -272,8 +273,9 @@ struct ERes2Builder {
       const int kp = stem.Kp;
       const Buf xo = x.buf;
       const int ld = x.ld;
+      int* flag = b.exact ? nullptr : m.range_flag;
       b.step("stem", [=](const Ctx& c) {
-        return launch_stem_conv3x3(c.in, B, T, F, w, bias, mc, ACT_RELU, kp, c.resolve(xo), ld, c.stream);
+        return launch_stem_conv3x3(c.in, B, T, F, w, bias, mc, ACT_RELU, kp, c.resolve(xo), ld, c.stream, nullptr, flag);
       });
     }
     // ---- scratch for the block internals, sized by the largest layer

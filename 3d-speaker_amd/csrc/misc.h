@@ -6,7 +6,10 @@ namespace spk {
 
 // vlen (optional, ragged batches): valid frames per utterance; outputs past them are 0
 hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const float* w, const float* bias, int cout,
-                               int act, int wstride, float* out, int ldo, hipStream_t s, const int* vlen = nullptr);
+                               int act, int wstride, float* out, int ldo, hipStream_t s, const int* vlen = nullptr,
+                               int* range_flag = nullptr);
+// range guard on a model input (common.h kRangeLimit): flag |= 1 if any |x[i]| >= 2^15
+hipError_t launch_range_check(const float* x, size_t n, int* flag, hipStream_t s);
 // fp32 -> (hi, lo) fp16 planes for the split-fp16 MFMA GEMM: hi = fp16(w),
 // lo = fp16((w - hi) * 2^11) (conv_gemm.hip, "fp16x3").
 hipError_t launch_split_f16(const float* w, uint16_t* hi, uint16_t* lo, size_t n, hipStream_t s);

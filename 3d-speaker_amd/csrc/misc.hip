@@ -1,3 +1,4 @@
+#include <algorithm>
 // Small bandwidth-bound kernels around the implicit-GEMM convs, gfx950:
 //  * stem conv 3x3, 1 -> Cout channels, reading Fbank features [B, T, F] directly (the
 //    reference's permute(0,2,1).unsqueeze(1) is folded into the index math), folded BN
@@ -15,7 +16,7 @@ namespace {
 __global__ void __launch_bounds__(256)
 stem_conv3x3_kernel(const float* __restrict__ feats, int B, int T, int F, const float* __restrict__ w,
                     const float* __restrict__ bias, int cout, int act, int wstride, float* __restrict__ out,
-                    int ldo, const int* __restrict__ vlen) {
+                    int ldo, const int* __restrict__ vlen, int* range_flag) {
   // thread -> (pixel, 16 output channels); pixel = (b, f, t) of the (F, T) image.  Weights and
   // bias are staged in LDS once per block; 32-bit index math only.
   __shared__ float ws[128 * 9];
@@ -25,6 +26,7 @@ stem_conv3x3_kernel(const float* __restrict__ feats, int B, int T, int F, const 
   __syncthreads();
   const int groups = cout / 16;
   const int total = B * F * T * groups;
+  float amax = 0.f;                                  // range guard (common.h)
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const int g = e % groups;
     const int pix = e / groups;
@@ -55,10 +57,20 @@ stem_conv3x3_kernel(const float* __restrict__ feats, int B, int T, int F, const 
         for (int k = 0; k < 9; ++k) acc = fmaf(in[k], ws[c * 9 + k], acc);
         acc += bs[c];
         ov[j] = dead ? 0.f : (act == ACT_RELU ? fmaxf(acc, 0.f) : acc);
+        amax = fmaxf(amax, fabsf(ov[j]));
       }
       *reinterpret_cast<float4*>(op + q * 4) = o;
     }
   }
+  range_note(range_flag, amax);
+}
+
+// range guard on a model input (common.h): grid-stride max |x| of n floats
+__global__ void __launch_bounds__(256) range_check_kernel(const float* __restrict__ x, size_t n, int* flag) {
+  float amax = 0.f;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    amax = fmaxf(amax, fabsf(x[i]));
+  range_note(flag, amax);
 }
 
 // x: [B, H, W, C] (pixel stride ld).  out: [B, 2*H*C]: mean at [h*C + c], std at [H*C + h*C + c].
@@ -90,13 +102,21 @@ tstp_kernel(const float* __restrict__ x, int B, int H, int W, int C, int ld, flo
 }  // namespace
 
 hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const float* w, const float* bias, int cout,
-                               int act, int wstride, float* out, int ldo, hipStream_t s, const int* vlen) {
+                               int act, int wstride, float* out, int ldo, hipStream_t s, const int* vlen,
+                               int* range_flag) {
   if (cout % 16 || cout > 128 || ldo % 4 || (long long)B * F * T * (cout / 16) >= (1LL << 31))
     return hipErrorInvalidValue;
   const long long total = (long long)B * F * T * (cout / 16);
   const int blocks = (int)std::min<long long>((total + 255) / 256, 65536);
   hipLaunchKernelGGL(stem_conv3x3_kernel, dim3(blocks), dim3(256), 0, s, feats, B, T, F, w, bias, cout, act, wstride, out,
-                     ldo, vlen);
+                     ldo, vlen, range_flag);
+  return hipGetLastError();
+}
+
+hipError_t launch_range_check(const float* x, size_t n, int* flag, hipStream_t s) {
+  if (!flag || n == 0) return hipSuccess;
+  const size_t blocks = std::min<size_t>(1024, (n + 255) / 256);
+  hipLaunchKernelGGL(range_check_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, n, flag);
   return hipGetLastError();
 }
 

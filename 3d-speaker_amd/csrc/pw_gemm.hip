@@ -149,14 +149,18 @@ pw_gemm_x3_kernel(const ConvDesc d) {
       accx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, accx, 0, 0, 0);
     }
     if (nok) {
+      float amax = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = mbase + (r & 3) + 8 * (r >> 2);
         if (m >= M) continue;
         float v = apply_act(acc[r] + accx[r] * (1.0f / 2048.0f) + bias + res[r], d.act);
         if (d.post_scale) v = v * ps + pt;
-        ocol[(size_t)m * d.ldo] = row_masked(d, m) ? 0.f : apply_act(v, d.act2);
+        v = row_masked(d, m) ? 0.f : apply_act(v, d.act2);
+        amax = fmaxf(amax, fabsf(v));
+        ocol[(size_t)m * d.ldo] = v;
       }
+      range_note(d.range_flag, amax);
     }
   };
 

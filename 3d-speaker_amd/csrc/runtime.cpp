@@ -118,6 +118,7 @@ const Packed& Model::pack(const std::string& name, const ChanMap& out, const std
   Packed p;
   p.N = N; p.K = K; p.Kp = Kp; p.has_bias = has_bias;
   std::vector<float> wf(wd.begin(), wd.end()), bf(bd.begin(), bd.end());
+  for (float v : wf) gemm_wmax = std::max(gemm_wmax, std::fabs(v));   // range guard (common.h)
   p.w_off = put(wf);
   p.b_off = put(bf);
   return packed.emplace(name, p).first->second;
@@ -161,8 +162,9 @@ void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const C
   if (!plan) return;
   d.N = p.N; d.K = p.K; d.Kp = p.Kp;
   d.w = m.dptr(p.w_off);
-  d.wh = m.dhi(p.w_off);
-  d.wl = m.dlo(p.w_off);
+  d.wh = exact ? nullptr : m.dhi(p.w_off);   // no split planes: the exact-fp32 kernels are chosen
+  d.wl = exact ? nullptr : m.dlo(p.w_off);
+  d.range_flag = exact ? nullptr : m.range_flag;
   d.bias = (use_bias && p.has_bias) ? m.dptr(p.b_off) : nullptr;
   const int M = d.nimg * d.Ho * d.Wo;
   // split-K for skinny, deep GEMMs (e.g. the 20480 -> 192 embedding layer)
@@ -250,15 +252,32 @@ spk::Plan::~Plan() {
 
 namespace {
 
-Plan* get_plan(spk_model_t* h, int B, int T, bool ragged = false) {
+Plan* get_plan(spk_model_t* h, int B, int T, bool ragged = false, bool exact = false) {
   std::lock_guard<std::mutex> lk(h->m.mu);
-  auto key = std::make_pair(B, ragged ? -T : T);
+  exact = exact || h->m.force_exact || !conv_use_x3();
+  const auto key = std::make_tuple(B, T, (int)ragged, (int)exact);
+  h->m.plan_use[key] = ++h->m.plan_clock;
   auto it = h->m.plans.find(key);
   if (it != h->m.plans.end()) return it->second.get();
   if (ragged && h->m.cfg.arch != SPK_ARCH_CAMPPLUS && h->m.cfg.arch != SPK_ARCH_ECAPA)
     throw SpkError(SPK_E_UNSUPPORTED, "per-utterance lengths are implemented for CAM++ and ECAPA-TDNN only");
+  if (h->m.plans.size() >= Model::kMaxPlans) {
+    // evict the least recently used plan; its graphs may still run on some stream
+    auto victim = h->m.plans.begin();
+    for (auto p = h->m.plans.begin(); p != h->m.plans.end(); ++p)
+      if (h->m.plan_use[p->first] < h->m.plan_use[victim->first]) victim = p;
+    (void)hipDeviceSynchronize();
+    h->m.plan_use.erase(victim->first);
+    h->m.plans.erase(victim);
+  }
   auto plan = std::make_unique<Plan>();
-  Builder b(h->m, plan.get(), B, ragged);
+  Builder b(h->m, plan.get(), B, ragged, exact);
+  if (!exact) {
+    // fp16x3 range guard on the model input (common.h)
+    const size_t n = (size_t)B * T * h->m.cfg.feat_dim;
+    int* flag = h->m.range_flag;
+    b.step("range_in", [n, flag](const Ctx& c) { return launch_range_check(c.in, n, flag, c.stream); });
+  }
   switch (h->m.cfg.arch) {
     case SPK_ARCH_ERES2NETV2: build_eres2net(b, T, true); break;
     case SPK_ARCH_ERES2NET: build_eres2net(b, T, false); break;
@@ -367,13 +386,17 @@ int spk_model_create(const spk_model_config_t* cfg, const spk_weight_t* weights,
     }
     // pack every layer (a plan-less build), then upload once
     {
-      Builder b(h->m, nullptr, 1);
-      switch (cfg->arch) {
-        case SPK_ARCH_ERES2NETV2: build_eres2net(b, 200, true); break;
-        case SPK_ARCH_ERES2NET: build_eres2net(b, 200, false); break;
-        case SPK_ARCH_ECAPA: build_ecapa(b, 200); break;
-        case SPK_ARCH_CAMPPLUS: build_campplus(b, 200); break;
-        default: set_error("spk_model_create: unknown arch"); return SPK_E_UNSUPPORTED;
+      // pack every weight either plan reads (the fused fp16x3 plan and the exact-fp32 one of
+      // the range guard may use different layouts of the same tensor)
+      for (const bool exact : {false, true}) {
+        Builder b(h->m, nullptr, 1, false, exact);
+        switch (cfg->arch) {
+          case SPK_ARCH_ERES2NETV2: build_eres2net(b, 200, true); break;
+          case SPK_ARCH_ERES2NET: build_eres2net(b, 200, false); break;
+          case SPK_ARCH_ECAPA: build_ecapa(b, 200); break;
+          case SPK_ARCH_CAMPPLUS: build_campplus(b, 200); break;
+          default: set_error("spk_model_create: unknown arch"); return SPK_E_UNSUPPORTED;
+        }
       }
     }
     h->m.dweights_bytes = h->m.arena.size() * sizeof(float);
@@ -396,6 +419,13 @@ int spk_model_create(const spk_model_config_t* cfg, const spk_weight_t* weights,
         return rc;
       if (int rc = hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize")) return rc;
     }
+    {
+      // fp16x3 range guard (common.h): a weight past fp16's range forces the exact path;
+      // the activation flag word is cleared once here and by spk_model_range_check
+      h->m.force_exact = !(h->m.gemm_wmax < 65504.0f);   // the split GEMM operands only
+      if (int rc = hip_check(hipMalloc(&h->m.range_flag, 256), "hipMalloc(range flag)")) return rc;
+      if (int rc = hip_check(hipMemset(h->m.range_flag, 0, 256), "hipMemset(range flag)")) return rc;
+    }
     h->m.uploaded = true;
     h->m.arena.clear();
     h->m.arena.shrink_to_fit();
@@ -409,6 +439,7 @@ int spk_model_destroy(spk_model_t* model) {
   if (!model) return SPK_OK;
   if (model->m.dweights) (void)hipFree(model->m.dweights);
   if (model->m.dsplit) (void)hipFree(model->m.dsplit);
+  if (model->m.range_flag) (void)hipFree(model->m.range_flag);
   delete model;
   return SPK_OK;
 }
@@ -419,7 +450,7 @@ int spk_model_workspace_bytes(spk_model_t* model, int32_t B, int32_t T, size_t* 
       set_error("spk_model_workspace_bytes: invalid argument");
       return SPK_E_INVALID;
     }
-    *bytes = get_plan(model, B, T)->ws_bytes;
+    *bytes = std::max(get_plan(model, B, T)->ws_bytes, get_plan(model, B, T, false, true)->ws_bytes);
     return SPK_OK;
   });
 }
@@ -505,7 +536,8 @@ static int run_graph(const char* fn, spk_model_t* model, Plan* plan, const float
 }
 
 static int run_forward(const char* fn, spk_model_t* model, const float* feats, int32_t B, int32_t T,
-                       const int32_t* lengths, void* workspace, size_t workspace_bytes, float* emb_out, void* stream) {
+                       const int32_t* lengths, void* workspace, size_t workspace_bytes, float* emb_out, void* stream,
+                       bool exact = false) {
   if (!model || !feats || !emb_out || B <= 0 || T <= 0) {
     set_error(std::string(fn) + ": invalid argument");
     return SPK_E_INVALID;
@@ -516,7 +548,7 @@ static int run_forward(const char* fn, spk_model_t* model, const float* feats, i
     set_error(std::string(fn) + ": handle belongs to another device");
     return SPK_E_DEVICE;
   }
-  Plan* plan = get_plan(model, B, T, lengths != nullptr);
+  Plan* plan = get_plan(model, B, T, lengths != nullptr, exact);
   if (workspace_bytes < plan->ws_bytes || (plan->ws_bytes && !workspace)) {
     set_error(std::string(fn) + ": workspace too small (need " + std::to_string(plan->ws_bytes) + " bytes)");
     return SPK_E_WORKSPACE;
@@ -548,7 +580,7 @@ int spk_model_workspace_bytes_lengths(spk_model_t* model, int32_t B, int32_t T, 
       set_error("spk_model_workspace_bytes_lengths: invalid argument");
       return SPK_E_INVALID;
     }
-    *bytes = get_plan(model, B, T, ragged != 0)->ws_bytes;
+    *bytes = std::max(get_plan(model, B, T, ragged != 0)->ws_bytes, get_plan(model, B, T, ragged != 0, true)->ws_bytes);
     return SPK_OK;
   });
 }
@@ -558,6 +590,32 @@ int spk_model_forward_lengths(spk_model_t* model, const float* feats, int32_t B,
   return guarded([&]() -> int {
     return run_forward("spk_model_forward_lengths", model, feats, B, T, lengths, workspace, workspace_bytes, emb_out,
                        stream);
+  });
+}
+
+int spk_model_forward_exact(spk_model_t* model, const float* feats, int32_t B, int32_t T, const int32_t* lengths,
+                            void* workspace, size_t workspace_bytes, float* emb_out, void* stream) {
+  return guarded([&]() -> int {
+    return run_forward("spk_model_forward_exact", model, feats, B, T, lengths, workspace, workspace_bytes, emb_out,
+                       stream, true);
+  });
+}
+
+int spk_model_range_check(spk_model_t* model, void* stream, int32_t* overflowed) {
+  return guarded([&]() -> int {
+    if (!model || !overflowed || !model->m.range_flag) {
+      set_error("spk_model_range_check: invalid argument");
+      return SPK_E_INVALID;
+    }
+    const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int v = 0;
+    if (int rc = hip_check(hipMemcpyAsync(&v, model->m.range_flag, sizeof(int), hipMemcpyDeviceToHost, s), "range flag"))
+      return rc;
+    if (int rc = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize")) return rc;
+    if (v)
+      if (int rc = hip_check(hipMemsetAsync(model->m.range_flag, 0, sizeof(int), s), "range flag reset")) return rc;
+    *overflowed = v != 0;
+    return SPK_OK;
   });
 }
 

@@ -5,6 +5,7 @@
 #include <memory>
 #include <mutex>
 #include <stdexcept>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -104,7 +105,15 @@ struct Model {
   size_t dweights_bytes = 0;
   uint16_t* dsplit = nullptr;                     // fp16 hi plane then lo plane of the whole arena
   std::map<std::string, Packed> packed;
-  std::map<std::pair<int, int>, std::unique_ptr<Plan>> plans;   // key (B, T) ; ragged plans use -T
+  // launch plans by (B, T, ragged, exact); at most kMaxPlans are kept (least recently used
+  // evicted: variable-length callers would otherwise grow plans and graphs without bound)
+  std::map<std::tuple<int, int, int, int>, std::unique_ptr<Plan>> plans;
+  std::map<std::tuple<int, int, int, int>, uint64_t> plan_use;
+  uint64_t plan_clock = 0;
+  static constexpr size_t kMaxPlans = 24;
+  int* range_flag = nullptr;                      // device word of the fp16x3 range guard (common.h)
+  bool force_exact = false;                       // a packed weight is out of fp16 range: exact path only
+  float gemm_wmax = 0.f;                          // max |w| over the packed GEMM weights
   std::mutex mu;
   bool uploaded = false;
 
@@ -133,7 +142,9 @@ struct Builder {
   double macs_per_utt = 0;   // algorithmic conv/linear MACs for this (T)
   double macs_at_last_step = 0;
   bool ragged = false;       // per-utterance lengths (Buf::LEN) mask the time axis
-  Builder(Model& mm, Plan* p, int b, bool rg = false) : m(mm), plan(p), B(b), ragged(rg) {}
+  bool exact = false;        // exact-fp32 MFMA kernels only (no fp16x3 split anywhere)
+  Builder(Model& mm, Plan* p, int b, bool rg = false, bool ex = false) : m(mm), plan(p), B(b), ragged(rg), exact(ex) {}
+  bool x3() const { return !exact && conv_use_x3(); }
   Buf alloc(size_t floats);
   void step(const std::string& name, Step s, const std::string& kernel = "", double bytes = 0.0);
   // emit an implicit-GEMM conv; pointers of `d` are taken from the Bufs

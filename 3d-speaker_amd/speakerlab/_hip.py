@@ -64,6 +64,9 @@ SYMBOLS = {
     'spk_model_forward_lengths': (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_size_t, _P,
                                                  _P]),
     'spk_model_flops': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_double)]),
+    'spk_model_range_check': (ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_int32)]),
+    'spk_model_forward_exact': (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_size_t, _P,
+                                               _P]),
     'spk_model_plan_size': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
     'spk_model_plan_step': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p,
                                            ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32,
@@ -229,6 +232,7 @@ class NativeModel:
                    'spk_model_create')
         self.handle = handle
         self._ws: Optional[torch.Tensor] = None
+        self.last_forward_exact = False
 
     def __del__(self):
         h = getattr(self, 'handle', None)
@@ -326,6 +330,18 @@ class NativeModel:
                                                        self._ws.data_ptr(), self._ws.numel(), out.data_ptr(),
                                                        _stream(self.device)),
                        'spk_model_forward_lengths')
+            # fp16x3 range guard (include/spk_hip.h): an activation reached fp16's range ->
+            # the same forward again on the exact-fp32 kernels
+            flag = ctypes.c_int32(0)
+            _check(lib().spk_model_range_check(self.handle, _stream(self.device), ctypes.byref(flag)),
+                   'spk_model_range_check')
+            self.last_forward_exact = bool(flag.value)
+            if flag.value:
+                _check(lib().spk_model_forward_exact(self.handle, feats.data_ptr(), B, T,
+                                                     None if lengths is None else lengths.data_ptr(),
+                                                     self._ws.data_ptr(), self._ws.numel(), out.data_ptr(),
+                                                     _stream(self.device)),
+                       'spk_model_forward_exact')
         return out
 
 

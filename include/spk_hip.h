@@ -121,6 +121,18 @@ int spk_model_workspace_bytes_lengths(spk_model_t* model, int32_t B, int32_t T, 
 int spk_model_forward_lengths(spk_model_t* model, const float* feats, int32_t B, int32_t T, const int32_t* lengths,
                               void* workspace, size_t workspace_bytes, float* emb_out, void* stream);
 
+/* fp16x3 range guard.  The default kernels represent every GEMM operand as two fp16 values
+ * (fp32-accurate, csrc/conv_gemm.hip); a value at or past fp16's range (65504) would
+ * saturate.  Every producer of an unbounded activation (and the input check) sets a device
+ * flag of the handle when a value reaches 2^15; spk_model_range_check() synchronises the
+ * stream, reports and clears it, and spk_model_forward_exact() (same arguments as
+ * spk_model_forward_lengths, lengths may be NULL) runs the same forward on exact-fp32 MFMA
+ * kernels only.  A handle whose packed weights leave fp16's range always runs exact.  The
+ * workspace queries return the larger of the two plans' needs. */
+int spk_model_range_check(spk_model_t* model, void* stream, int32_t* overflowed);
+int spk_model_forward_exact(spk_model_t* model, const float* feats, int32_t B, int32_t T, const int32_t* lengths,
+                            void* workspace, size_t workspace_bytes, float* emb_out, void* stream);
+
 /* Algorithmic FLOPs per utterance of T frames (2 x conv/linear MACs). */
 int spk_model_flops(spk_model_t* model, int32_t T, double* flops);
 

@@ -87,7 +87,11 @@ hipError_t launch_conv(const ConvDesc& d, hipStream_t) {
       const float* w = d.w + (size_t)n * d.Kp;
       double acc = 0.0;
       for (int k = 0; k < d.Kp; ++k) acc += (double)a[k] * w[k];
-      *out_at(d, m, n) = epilogue(d, m, n, (float)acc);
+      {
+        const float o = epilogue(d, m, n, (float)acc);
+        if (d.range_flag && std::fabs(o) >= kRangeLimit) *d.range_flag |= 1;
+        *out_at(d, m, n) = o;
+      }
     }
   }
   return hipSuccess;
@@ -126,8 +130,17 @@ hipError_t launch_aff_x3(const AffDesc& a, hipStream_t) {
 // the emulated GEMM reads the fp32 weights; the split planes are not needed on the host
 hipError_t launch_split_f16(const float*, uint16_t*, uint16_t*, size_t, hipStream_t) { return hipSuccess; }
 
+static void emu_range_note(int* flag, float v) {   // common.h range guard
+  if (flag && std::fabs(v) >= kRangeLimit) *flag |= 1;
+}
+
+hipError_t launch_range_check(const float* x, size_t n, int* flag, hipStream_t) {
+  for (size_t i = 0; i < n; ++i) emu_range_note(flag, x[i]);
+  return hipSuccess;
+}
+
 hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const float* w, const float* bias, int cout,
-                               int act, int wstride, float* out, int ldo, hipStream_t, const int* vlen) {
+                               int act, int wstride, float* out, int ldo, hipStream_t, const int* vlen, int* range_flag) {
   for (int b = 0; b < B; ++b) {
     const int Tb = vlen ? vlen[b] : T;
     for (int f = 0; f < F; ++f)
@@ -140,7 +153,9 @@ hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const fl
               if (ff >= 0 && ff < F && tt >= 0 && tt < Tb) acc += (double)feats[((size_t)b * T + tt) * F + ff] * w[c * wstride + dy * 3 + dx];
             }
           float v = (float)acc + bias[c];
-          out[(((size_t)b * F + f) * T + t) * ldo + c] = t >= Tb ? 0.f : (act == ACT_RELU ? std::fmax(v, 0.f) : v);
+          const float o = t >= Tb ? 0.f : (act == ACT_RELU ? std::fmax(v, 0.f) : v);
+          emu_range_note(range_flag, o);
+          out[(((size_t)b * F + f) * T + t) * ldo + c] = o;
         }
   }
   return hipSuccess;
@@ -288,6 +303,8 @@ hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
 hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
 hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
 hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) { std::memset(p, v, n); return hipSuccess; }
+hipError_t hipMemset(void* p, int v, size_t n) { std::memset(p, v, n); return hipSuccess; }
+hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
 // the spectral entry points (csrc/spectral.hip) are not emulated: their parity is a -m gpu test
 int spk_spectral_laplacian(const float*, int64_t, int64_t, int32_t, float*, int64_t, void*, size_t, void*) {
   return SPK_E_UNSUPPORTED;

@@ -76,8 +76,9 @@ def test_emulated_ragged_campplus_matches_per_utterance(arch):
 
 def test_step_bytes_priced_per_conv():
     """Per-step algorithmic bytes (the byte side of bench.py's per-launch roofline): every
-    conv step is priced, and ERes2NetV2 layer1.1.conv3 (1x1, 56 -> 128 channels, residual)
-    is exactly input + weights + output + residual, fp32."""
+    conv step is priced; ERes2NetV2 layer2.1.conv3 (1x1, 104 -> 256 channels, residual) is
+    exactly input + weights + output + residual, fp32, and the fused stage-1 block
+    layer1.1.fused is its input + output + the four packed weight matrices."""
     m = helpers.loaded_module('eres2netv2')
     em = EmuModel(m)
     B, T = 2, 40
@@ -87,6 +88,9 @@ def test_step_bytes_priced_per_conv():
     for (name, _, kern), by in zip(steps, nbytes):
         if kern.startswith(('conv_gemm', 'conv3x3', 'pw_gemm')):
             assert by > 0, name
-    i = [name for name, _, _ in steps].index('layer1.1.conv3')
+    names = [name for name, _, _ in steps]
+    px2 = B * 40 * (T // 2)
+    assert nbytes[names.index("layer2.1.conv3")] == 4.0 * (px2 * 104 + 256 * 104 + px2 * 256 + px2 * 256)
     px = B * 80 * T
-    assert nbytes[i] == 4.0 * (px * 56 + 128 * 56 + px * 128 + px * 128)
+    w = 64 * 128 + 2 * 32 * 288 + 128 * 64
+    assert nbytes[names.index('layer1.1.fused')] == 8.0 * px * 128 + 4.0 * w
