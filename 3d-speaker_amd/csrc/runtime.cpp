@@ -283,6 +283,8 @@ Plan* get_plan(spk_model_t* h, int B, int T, bool ragged = false, bool exact = f
     case SPK_ARCH_ERES2NET: build_eres2net(b, T, false); break;
     case SPK_ARCH_ECAPA: build_ecapa(b, T); break;
     case SPK_ARCH_CAMPPLUS: build_campplus(b, T); break;
+    case SPK_ARCH_RESNET: build_resnet(b, T, false); break;
+    case SPK_ARCH_RES2NET: build_resnet(b, T, true); break;
     default: throw SpkError(SPK_E_UNSUPPORTED, "unknown arch");
   }
   // staging regions for graph replay (input features, per-utterance lengths, embeddings)
@@ -395,6 +397,8 @@ int spk_model_create(const spk_model_config_t* cfg, const spk_weight_t* weights,
           case SPK_ARCH_ERES2NET: build_eres2net(b, 200, false); break;
           case SPK_ARCH_ECAPA: build_ecapa(b, 200); break;
           case SPK_ARCH_CAMPPLUS: build_campplus(b, 200); break;
+          case SPK_ARCH_RESNET: build_resnet(b, 200, false); break;
+          case SPK_ARCH_RES2NET: build_resnet(b, 200, true); break;
           default: set_error("spk_model_create: unknown arch"); return SPK_E_UNSUPPORTED;
         }
       }
@@ -467,6 +471,8 @@ int spk_model_flops(spk_model_t* model, int32_t T, double* flops) {
       case SPK_ARCH_ERES2NET: build_eres2net(b, T, false); break;
       case SPK_ARCH_ECAPA: build_ecapa(b, T); break;
       case SPK_ARCH_CAMPPLUS: build_campplus(b, T); break;
+      case SPK_ARCH_RESNET: build_resnet(b, T, false); break;
+      case SPK_ARCH_RES2NET: build_resnet(b, T, true); break;
       default: return SPK_E_UNSUPPORTED;
     }
     *flops = 2.0 * b.macs_per_utt;

@@ -158,6 +158,7 @@ struct Builder {
 void build_eres2net(Builder& b, int T, bool v2);
 void build_ecapa(Builder& b, int T);
 void build_campplus(Builder& b, int T);
+void build_resnet(Builder& b, int T, bool res2);
 
 void set_error(const std::string& msg);
 

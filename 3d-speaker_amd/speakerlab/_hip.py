@@ -21,6 +21,8 @@ ARCH_ERES2NETV2 = 1
 ARCH_ERES2NET = 2
 ARCH_ECAPA = 3
 ARCH_CAMPPLUS = 4
+ARCH_RESNET = 5
+ARCH_RES2NET = 6
 
 
 class spk_weight_t(ctypes.Structure):

@@ -50,6 +50,8 @@ extern "C" {
 #define SPK_ARCH_ERES2NET 2    /* speakerlab.models.eres2net.ERes2Net.ERes2Net     */
 #define SPK_ARCH_ECAPA 3       /* speakerlab.models.ecapa_tdnn.ECAPA_TDNN.ECAPA_TDNN */
 #define SPK_ARCH_CAMPPLUS 4    /* speakerlab.models.campplus.DTDNN.CAMPPlus         */
+#define SPK_ARCH_RESNET 5      /* speakerlab.models.resnet.ResNet.ResNet (BasicBlock, TSTP) */
+#define SPK_ARCH_RES2NET 6     /* speakerlab.models.res2net.Res2Net.Res2Net (TSTP)  */
 
 typedef struct spk_model spk_model_t;
 

@@ -14,6 +14,8 @@ layout) and restates the reference forward op for op with ``torch.nn.functional`
 * TSTP         — ``speakerlab/models/eres2net/pooling_layers.py:38-55``
 * ECAPA_TDNN   — ``speakerlab/models/ecapa_tdnn/ECAPA_TDNN.py:29-463``
 * CAMPPlus     — ``speakerlab/models/campplus/DTDNN.py:13-115``, ``layers.py:10-253``
+* ResNet34     — ``speakerlab/models/resnet/ResNet.py:15-113``
+* Res2Net      — ``speakerlab/models/res2net/Res2Net.py:17-147``
 
 It is pinned against golden embeddings produced by the reference modules themselves
 (``tests/golden/make_golden.py``) in ``tests/test_oracle_models.py``.
@@ -130,6 +132,67 @@ def eres2net_forward(sd: SD, x, m_channels=32, base_width=32, scale=2, num_block
     if two_emb_layer:
         emb = F.linear(_bn(F.relu(emb), sd, 'seg_bn_1'), sd['seg_2.weight'], sd['seg_2.bias'])
     return emb
+
+
+# ----------------------------------------------------------------------------- ResNet / Res2Net
+def _stem(sd: SD, x):
+    x = x.permute(0, 2, 1).unsqueeze(1)
+    return F.relu(_bn(F.conv2d(x, sd['conv1.weight'], padding=1), sd, 'bn1'))
+
+
+def _head(sd: SD, out, two_emb_layer):
+    emb = F.linear(_tstp(out), sd['seg_1.weight'], sd['seg_1.bias'])
+    if two_emb_layer:
+        emb = F.linear(_bn(F.relu(emb), sd, 'seg_bn_1'), sd['seg_2.weight'], sd['seg_2.bias'])
+    return emb
+
+
+def _shortcut(sd: SD, p: str, x, stride):
+    if p + '.shortcut.0.weight' in sd:
+        return _bn(F.conv2d(x, sd[p + '.shortcut.0.weight'], stride=stride), sd, p + '.shortcut.1')
+    return x
+
+
+def _resnet_block(sd: SD, p: str, x, stride):
+    """BasicBlock ResNet.py:30-35."""
+    out = F.relu(_bn(F.conv2d(x, sd[p + '.conv1.weight'], stride=stride, padding=1), sd, p + '.bn1'))
+    out = _bn(F.conv2d(out, sd[p + '.conv2.weight'], padding=1), sd, p + '.bn2')
+    return F.relu(out + _shortcut(sd, p, x, stride))
+
+
+def resnet_forward(sd: SD, x, num_blocks=(3, 4, 6, 3), two_emb_layer=True):
+    """ResNet.forward ResNet.py:86-101 (TSTP pooling)."""
+    out = _stem(sd, x)
+    for li, n in enumerate(num_blocks):
+        for b in range(n):
+            out = _resnet_block(sd, f'layer{li + 1}.{b}', out, (2 if li else 1) if b == 0 else 1)
+    return _head(sd, out, two_emb_layer)
+
+
+def _res2net_block(sd: SD, p: str, x, stride, width, scale):
+    """BasicBlockRes2Net Res2Net.py:59-87: the last split passes through to the concat."""
+    out = _htanh(_bn(F.conv2d(x, sd[p + '.conv1.weight'], stride=stride), sd, p + '.bn1'))
+    spx = torch.split(out, width, 1)
+    nums = scale - 1
+    outs = []
+    sp = None
+    for i in range(nums):
+        sp = spx[i] if i == 0 else sp + spx[i]
+        sp = _htanh(_bn(F.conv2d(sp, sd[f'{p}.convs.{i}.weight'], padding=1), sd, f'{p}.bns.{i}'))
+        outs.append(sp)
+    out = torch.cat(outs + [spx[nums]], 1)
+    out = _bn(F.conv2d(out, sd[p + '.conv3.weight']), sd, p + '.bn3')
+    return _htanh(out + _shortcut(sd, p, x, stride))
+
+
+def res2net_forward(sd: SD, x, m_channels=32, base_width=32, scale=2, num_blocks=(3, 4, 6, 3), two_emb_layer=False):
+    """Res2Net.forward Res2Net.py:128-147 (TSTP pooling)."""
+    out = _stem(sd, x)
+    for li, n in enumerate(num_blocks):
+        width = int(math.floor(m_channels * (2 ** li) * (base_width / 64.0)))
+        for b in range(n):
+            out = _res2net_block(sd, f'layer{li + 1}.{b}', out, (2 if li else 1) if b == 0 else 1, width, scale)
+    return _head(sd, out, two_emb_layer)
 
 
 # ----------------------------------------------------------------------------- ECAPA
@@ -304,6 +367,8 @@ ARCHS = {
     'campplus_192': (campplus_forward, dict(feat_dim=80, embedding_size=192)),
     'eres2net_base': (lambda sd, x: eres2net_forward(sd, x, m_channels=32), dict(feat_dim=80, embedding_size=512,
                                                                                   m_channels=32)),
+    'resnet34': (resnet_forward, dict(feat_dim=80, embedding_size=192)),
+    'res2net': (res2net_forward, dict(feat_dim=80, embedding_size=192)),
 }
 
 

@@ -54,6 +54,8 @@ from speakerlab.models.eres2net.ERes2Net import ERes2Net  # noqa: E402
 from speakerlab.models.eres2net.ERes2Net_huge import ERes2Net as ERes2NetHuge  # noqa: E402
 from speakerlab.models.ecapa_tdnn.ECAPA_TDNN import ECAPA_TDNN  # noqa: E402
 from speakerlab.models.campplus.DTDNN import CAMPPlus  # noqa: E402
+from speakerlab.models.resnet.ResNet import ResNet  # noqa: E402
+from speakerlab.models.res2net.Res2Net import Res2Net  # noqa: E402
 from speakerlab.utils import score_metrics  # noqa: E402
 
 ARCHS = {
@@ -66,6 +68,9 @@ ARCHS = {
     'eres2netv2_w24s4ep4': (ERes2NetV2, dict(feat_dim=80, embedding_size=192, baseWidth=24, scale=4, expansion=4)),
     'campplus_192': (CAMPPlus, dict(feat_dim=80, embedding_size=192)),
     'eres2net_base': (ERes2Net, dict(feat_dim=80, embedding_size=512, m_channels=32)),
+    # the ResNet family of speakerlab/models
+    'resnet34': (ResNet, dict(feat_dim=80, embedding_size=192)),
+    'res2net': (Res2Net, dict(feat_dim=80, embedding_size=192)),
 }
 
 # (batch, samples) per golden set: 2 s, 1.5 s, 1 s  ->  T = 198, 148, 98 frames
@@ -91,7 +96,10 @@ def calibrate(model):
 
 def main():
     torch.manual_seed(0)
+    only = sys.argv[1:]            # optional: regenerate these archs only (+ always the EER set)
     for arch, (cls, kw) in ARCHS.items():
+        if only and arch not in only:
+            continue
         model = cls(**kw)
         synthetic.load_synthetic_weights(model, seed=0)
         calibrate(model)

@@ -8,7 +8,7 @@ import torch
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 ARCHS = ['eres2netv2', 'eres2net_large', 'ecapa', 'campplus']
-VARIANTS = ['eres2net_huge', 'eres2netv2_w24s4ep4', 'campplus_192', 'eres2net_base']
+VARIANTS = ['eres2net_huge', 'eres2netv2_w24s4ep4', 'campplus_192', 'eres2net_base', 'resnet34', 'res2net']
 
 
 def product_module(arch):
@@ -36,6 +36,12 @@ def product_module(arch):
     if arch == 'eres2net_base':
         from speakerlab.models.eres2net.ERes2Net import ERes2Net
         return ERes2Net(feat_dim=80, embedding_size=512, m_channels=32)
+    if arch == 'resnet34':
+        from speakerlab.models.resnet.ResNet import ResNet
+        return ResNet(feat_dim=80, embedding_size=192)
+    if arch == 'res2net':
+        from speakerlab.models.res2net.Res2Net import Res2Net
+        return Res2Net(feat_dim=80, embedding_size=192)
     raise KeyError(arch)
 
 
