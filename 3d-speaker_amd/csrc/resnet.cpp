@@ -10,11 +10,10 @@
 //   * ResNet BasicBlock = two implicit-GEMM convs: conv1 3x3(stride) + bn1 + ReLU -> MID;
 //     conv2 3x3 + bn2 with the projection shortcut (1x1 stride conv + BN) K-concatenated as
 //     a second operand, or the identity added in the epilogue, then ReLU;
-//   * Res2Net block: conv1 1x1(stride) + bn1 + Hardtanh -> planar T1 slices; scale-1 chained
-//     3x3 convs (sp + spx addend in the loader) -> CAT slices; conv3 reads CAT and the
-//     passed-through last T1 slice as a K-concatenated second operand (one GEMM for the
-//     torch.cat); the projection shortcut is its own GEMM whose output the conv3 epilogue
-//     adds (identity blocks add the input).
+//   * Res2Net block (scale 2): conv1 1x1(stride) + bn1 + Hardtanh writes spx0 into Z1 and
+//     spx1 straight into its concat position in Z2; the 3x3 conv writes sp next to it, so
+//     torch.cat is free and conv3 reads one operand; the projection shortcut is its own GEMM
+//     whose output the conv3 epilogue adds (identity blocks add the input).
 #include <cmath>
 
 #include "misc.h"
@@ -46,7 +45,7 @@ struct ResBuilder {
   Builder& b;
   Model& m;
   bool res2;
-  Buf MID, T1, CAT, SC;
+  Buf MID, Z1, Z2, SC;
 
   ResBuilder(Builder& bb, bool r2) : b(bb), m(bb.m), res2(r2) {}
 
@@ -96,45 +95,42 @@ struct ResBuilder {
     return out;
   }
 
-  // ---- BasicBlockRes2Net (Res2Net.py:59-87): `scale - 1` chained 3x3 convs, last split passed through
+  // ---- BasicBlockRes2Net (Res2Net.py:59-87), scale 2: conv1 -> [spx0 | spx1];
+  //   sp = Ht(bn(conv3x3(spx0))); out = Ht(bn3(conv3(cat(sp, spx1))) + shortcut).
+  // conv1's split epilogue writes spx0 into Z1 and spx1 straight into the second half of
+  // Z2's rows (two output planes, one plane stride apart); the 3x3 conv writes sp into the
+  // first half of Z2, so conv3 reads the concat as ONE operand of 2 x wp channels.
   R4 res2block(const std::string& p, const R4& x, int stride, int planes, Buf outbuf) {
     const int scale = m.cfg.scale ? m.cfg.scale : 2, expansion = m.cfg.expansion ? m.cfg.expansion : 2;
+    if (scale != 2) throw SpkError(SPK_E_UNSUPPORTED, "Res2Net: the executor implements scale 2 (the reference default)");
     const double bw = m.cfg.base_width ? m.cfg.base_width : 32;
-    const int width = (int)std::floor(planes * (bw / 64.0)), nums = scale - 1, Cout = planes * expansion;
+    const int width = (int)std::floor(planes * (bw / 64.0)), Cout = planes * expansion;
     const int Ho = (x.H - 1) / stride + 1, Wo = (x.W - 1) / stride + 1;
-    const ChanMap xin = ChanMap::dense(x.C), sl = ChanMap::slices(width, scale), one = ChanMap::dense(width);
-    const int wp = sl.n_phys / scale, ldc = nums * wp;
-    const size_t plane = (size_t)b.B * Ho * Wo * wp;
+    const ChanMap xin = ChanMap::dense(x.C), sl = ChanMap::slices(width, 2), one = ChanMap::dense(width);
+    const int wp = sl.n_phys / 2, ldz = 2 * wp;
     const double px = (double)Ho * Wo;
     const Packed& c1 = m.pack(p + ".conv1", sl, {Part{p + ".conv1.weight", "", p + ".bn1", xin, 0, 0}}, x.C);
-    b.macs_per_utt += px * x.C * (double)width * scale;
+    b.macs_per_utt += px * x.C * (double)width * 2;
     if (b.plan) {
       ConvDesc d;
       d.nimg = b.B; d.Ho = Ho; d.Wo = Wo;
       d.s0 = src(x, x.C, 1, stride, 0);
-      d.ldo = wp; d.osplit = wp; d.oplane = (long long)plane;
+      d.ldo = ldz; d.osplit = wp;
+      d.oplane = (long long)((Z2.off - Z1.off) / sizeof(float)) + wp;   // plane 1 -> Z2[:, wp:]
       d.act = ACT_HTANH;
-      Builder::ConvIO io; io.s0 = x.buf; io.out = T1;
+      Builder::ConvIO io; io.s0 = x.buf; io.out = Z1;
       b.conv(p + ".conv1", d, c1, io);
     }
-    for (int i = 0; i < nums; ++i) {
-      const std::string ci = std::to_string(i);
-      const Packed& cv = m.pack(p + ".convs." + ci, one,
-                                {Part{p + ".convs." + ci + ".weight", "", p + ".bns." + ci, one, 0, 0}}, 9 * wp);
-      b.macs_per_utt += px * 9.0 * width * width;
-      if (b.plan) {
-        const R4 in{T1.at((size_t)i * plane), wp, Ho, Wo, wp};
-        ConvDesc d;
-        d.nimg = b.B; d.Ho = Ho; d.Wo = Wo;
-        d.s0 = src(in, wp, 3, 1, 1);
-        Builder::ConvIO io; io.s0 = in.buf; io.out = CAT.at((size_t)i * wp);
-        if (i > 0) {                                   // sp = sp + spx[i]
-          d.s0.ld2 = ldc;
-          io.s0b = CAT.at((size_t)(i - 1) * wp);
-        }
-        d.ldo = ldc; d.act = ACT_HTANH;
-        b.conv(p + ".convs." + ci, d, cv, io);
-      }
+    const Packed& cv = m.pack(p + ".convs.0", one, {Part{p + ".convs.0.weight", "", p + ".bns.0", one, 0, 0}}, 9 * wp);
+    b.macs_per_utt += px * 9.0 * width * width;
+    if (b.plan) {
+      const R4 in{Z1, ldz, Ho, Wo, wp};
+      ConvDesc d;
+      d.nimg = b.B; d.Ho = Ho; d.Wo = Wo;
+      d.s0 = src(in, wp, 3, 1, 1);
+      d.ldo = ldz; d.act = ACT_HTANH;
+      Builder::ConvIO io; io.s0 = Z1; io.out = Z2;
+      b.conv(p + ".convs.0", d, cv, io);
     }
     // shortcut: projection GEMM into SC (added by the conv3 epilogue) or the identity
     const bool sc = m.has(p + ".shortcut.0.weight");
@@ -154,22 +150,15 @@ struct ResBuilder {
         b.conv(p + ".shortcut", d, s, io);
       }
     }
-    // conv3 over cat(sp_0 .. sp_{nums-1}, spx[nums]): CAT slices K-concatenated with T1 plane `nums`
-    ChanMap cm = ChanMap::slices(width, nums);
-    const Packed& c3 = m.pack(p + ".conv3", om,
-                              {Part{p + ".conv3.weight", "", p + ".bn3", cm, 0, 0},
-                               Part{p + ".conv3.weight", "", p + ".bn3", one, nums * width, ldc}},
-                              ldc + wp);
-    b.macs_per_utt += px * (double)width * scale * Cout;
+    const Packed& c3 = m.pack(p + ".conv3", om, {Part{p + ".conv3.weight", "", p + ".bn3", sl, 0, 0}}, ldz);
+    b.macs_per_utt += px * (double)width * 2 * Cout;
     R4 out{outbuf, om.n_phys, Ho, Wo, om.n_phys};
     if (b.plan) {
-      const R4 cat{CAT, ldc, Ho, Wo, ldc};
-      const R4 last{T1.at((size_t)nums * plane), wp, Ho, Wo, wp};
+      const R4 cat{Z2, ldz, Ho, Wo, ldz};
       ConvDesc d;
       d.nimg = b.B; d.Ho = Ho; d.Wo = Wo;
-      d.s0 = src(cat, ldc, 1, 1, 0);
-      d.s1 = src(last, wp, 1, 1, 0);
-      Builder::ConvIO io; io.s0 = CAT; io.s1 = last.buf; io.out = outbuf;
+      d.s0 = src(cat, ldz, 1, 1, 0);
+      Builder::ConvIO io; io.s0 = Z2; io.out = outbuf;
       if (sc) {
         d.ldr = om.n_phys;
         io.res = SC;
@@ -202,7 +191,7 @@ struct ResBuilder {
       });
     }
     // ---- block scratch sized by the largest stage
-    size_t mid = 0, t1 = 0, cat = 0, scb = 0;
+    size_t mid = 0, z = 0, scb = 0;
     {
       int H = F, W = T;
       for (int li = 0; li < 4; ++li) {
@@ -211,18 +200,15 @@ struct ResBuilder {
         const int planes = mc << li;
         mid = std::max(mid, px * ChanMap::dense(planes).n_phys);
         if (res2) {
-          const int scale = m.cfg.scale ? m.cfg.scale : 2;
           const int width = (int)std::floor(planes * ((m.cfg.base_width ? m.cfg.base_width : 32) / 64.0));
-          const ChanMap sl = ChanMap::slices(width, scale);
-          t1 = std::max(t1, px * sl.n_phys);
-          cat = std::max(cat, px * (sl.n_phys / scale) * (scale - 1));
+          z = std::max(z, px * ChanMap::slices(width, 2).n_phys);
           scb = std::max(scb, px * ChanMap::dense(planes * expansion).n_phys);
         }
       }
     }
     if (res2) {
-      T1 = b.alloc(t1);
-      CAT = b.alloc(cat);
+      Z1 = b.alloc(z);
+      Z2 = b.alloc(z);
       SC = b.alloc(scb);
     } else {
       MID = b.alloc(mid);
