@@ -315,6 +315,14 @@ res2_block_kernel(const Res2Desc d) {
     __syncthreads();
     R2_STAMP(4);
 
+    // residual of the first half of the conv3 pixel tiles: requested now, in flight during convs.1
+    f32x4 res_a[4];
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) {
+      const int gy = min(y0 + pt, H - 1), gx = min(x0 + l16, W - 1);
+      res_a[pt] = *reinterpret_cast<const f32x4*>(xim + ((size_t)gy * W + gx) * C + 16 * wave + 4 * lq);
+    }
+
     // ================= 3. convs.1 on the output tile (2 pixel tiles per wave)
     {
       f32x4 acc[2], accx[2];
@@ -363,16 +371,23 @@ res2_block_kernel(const Res2Desc d) {
     R2_STAMP(5);
 
     // ================= 4. conv3 + bn3 + residual + Hardtanh -> out (8 pixel tiles per wave)
-    // residual of the conv3 epilogue: all requested before the first MFMA
-    f32x4 res[G::NT3][8];
+    // residual of the second half: requested before the first MFMA (the first half is in flight)
+    f32x4 res_b[4];
 #pragma unroll
-    for (int j = 0; j < G::NT3; ++j)
-#pragma unroll
-      for (int pt = 0; pt < 8; ++pt) {
-        const int gy = min(y0 + pt, H - 1), gx = min(x0 + l16, W - 1);
-        res[j][pt] = *reinterpret_cast<const f32x4*>(xim + ((size_t)gy * W + gx) * C + 16 * (wave + 8 * j) + 4 * lq);
-      }
-
+    for (int pt = 0; pt < 4; ++pt) {
+      const int gy = min(y0 + 4 + pt, H - 1), gx = min(x0 + l16, W - 1);
+      res_b[pt] = *reinterpret_cast<const f32x4*>(xim + ((size_t)gy * W + gx) * C + 16 * wave + 4 * lq);
+    }
+    // the next tile's first three input chunks, behind the residual (vmcnt retires in order,
+    // so the epilogue's wait for the residual does not wait for these)
+    if (t + nslot < t_hi) {
+      int im, ty0, tx0;
+      tile_origin(t + nslot, im, ty0, tx0);
+      const float* pn = d.x + (size_t)im * H * W * C;
+      load_chunk(0, pf[0], ty0, tx0, pn);
+      load_chunk(1, pf[1], ty0, tx0, pn);
+      load_chunk(2, pf[2], ty0, tx0, pn);
+    }
 #pragma unroll
     for (int j = 0; j < G::NT3; ++j) {
       const int n = 16 * (wave + 8 * j) + 4 * lq;
@@ -393,18 +408,10 @@ res2_block_kernel(const Res2Desc d) {
         if (gy < H && gx < W) {
           f32x4 v;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = htanh(acc[e] + accx[e] * kLo + b3v[j][e] + res[j][pt][e]);
+          for (int e = 0; e < 4; ++e) v[e] = htanh(acc[e] + accx[e] * kLo + b3v[j][e] + (pt < 4 ? res_a[pt][e] : res_b[pt - 4][e]));
           *reinterpret_cast<f32x4*>(d.out + (((size_t)img * H + gy) * W + gx) * C + n) = v;
         }
       }
-    }
-    if (t + nslot < t_hi) {                   // the next tile's first three input chunks
-      int im, ty0, tx0;
-      tile_origin(t + nslot, im, ty0, tx0);
-      const float* pn = d.x + (size_t)im * H * W * C;
-      load_chunk(0, pf[0], ty0, tx0, pn);
-      load_chunk(1, pf[1], ty0, tx0, pn);
-      load_chunk(2, pf[2], ty0, tx0, pn);
     }
     R2_STAMP(6);
     __syncthreads();                          // CAT reads done before the next tile's conv1
