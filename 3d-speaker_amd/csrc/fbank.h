@@ -14,6 +14,10 @@ struct FbankTables {
   int mel_len[128];         // number of bins with non-zero weight
   int mel_off[128];         // offset of its weights in mel_w
   double mel_w[4096];
+  int mel_nb;               // max mel_len rounded up to a multiple of 16
+  int mel_blk_nb[4];        // max mel_len over bands 32 b .. 32 b + 31, rounded up to a multiple of 4
+  double mel_wt[4096];      // dense zero-padded bank [t][m] = weight of bin mel_start[m] + t for
+                            // band m, t < mel_nb: a wave's lanes (consecutive bands) read one line
 };
 
 // Host-side construction (double precision).  Returns the number of mel weights used;
@@ -24,6 +28,6 @@ int build_fbank_tables(FbankTables* t, int n_mels, double sample_rate);
 // its t_max rows zeroed (a padded [n_utt, t_max, n_mels] batch); frame_off still gives frames_u
 hipError_t launch_fbank(const float* wav, const int64_t* wav_off, int n_utt, float* feats,
                         const int64_t* frame_off, int n_mels, int mean_nor, const FbankTables* tab,
-                        hipStream_t s, int t_max = 0);
+                        int mel_nb, hipStream_t s, int t_max = 0);
 
 }  // namespace spk

@@ -223,6 +223,7 @@ namespace {
 
 FbankTables* g_tables[64] = {nullptr};
 int g_tables_mels[64] = {0};
+int g_tables_nb[64] = {0};
 std::mutex g_tables_mu;
 
 template <class F>
@@ -323,6 +324,7 @@ static int fbank_impl(const float* wav, const int64_t* wav_offsets, int32_t n_ut
     if (int rc = hip_check(hipGetDevice(&dev), "hipGetDevice")) return rc;
     if (dev < 0 || dev >= 64) return SPK_E_DEVICE;
     FbankTables* tab = nullptr;
+    int mel_nb = 0;
     {
       std::lock_guard<std::mutex> lk(g_tables_mu);
       if (!g_tables[dev] || g_tables_mels[dev] != n_mels) {
@@ -338,10 +340,12 @@ static int fbank_impl(const float* wav, const int64_t* wav_offsets, int32_t n_ut
         if (int rc = hip_check(hipMemcpy(g_tables[dev], &host, sizeof(host), hipMemcpyHostToDevice), "hipMemcpy"))
           return rc;
         g_tables_mels[dev] = n_mels;
+        g_tables_nb[dev] = host.mel_nb;
       }
       tab = g_tables[dev];
+      mel_nb = g_tables_nb[dev];
     }
-    return hip_check(launch_fbank(wav, wav_offsets, n_utt, feats, frame_offsets, n_mels, mean_nor, tab,
+    return hip_check(launch_fbank(wav, wav_offsets, n_utt, feats, frame_offsets, n_mels, mean_nor, tab, mel_nb,
                                   reinterpret_cast<hipStream_t>(stream), t_max),
                      "fbank launch");
   });

@@ -141,6 +141,41 @@ def roofline(model, feats, device, traffic_json):
     }
 
 
+def fbank_roofline(wavs, device, reps=20):
+    """The Fbank front end on its own: HIP events around `reps` back-to-back spk_fbank_f32
+    calls (frames kernel + mean-normalisation kernel) on torch's current stream, the stream
+    the library launches on.  Algorithmic bytes per utterance = 4 B per input sample + 4 B
+    per output feature (every operand once)."""
+    from speakerlab import _hip
+    B, L = wavs.shape
+    nfr = _hip.num_frames(L)
+    offs = torch.tensor([[i * L for i in range(B + 1)], [i * nfr for i in range(B + 1)]],
+                        dtype=torch.int64, device=device)
+    feats = torch.empty(B * nfr, 80, device=device)
+    lib, stream = _hip.lib(), torch.cuda.current_stream(device).cuda_stream
+
+    def call():
+        rc = lib.spk_fbank_f32(wavs.data_ptr(), offs[0].data_ptr(), B, feats.data_ptr(), offs[1].data_ptr(),
+                               80, 1, stream)
+        assert rc == 0, 'spk_fbank_f32 failed'
+    for _ in range(3):
+        call()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        call()
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    nbytes = B * (4 * L + 4 * 80 * nfr)
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return {'kernel': 'fbank_frames_kernel + fbank_cmn_kernel', 'bound': 'hbm', 'achieved': round(gbs, 1),
+            'peak': PEAK_HBM_GBS, 'unit': 'GB/s', 'frac': round(gbs / PEAK_HBM_GBS, 4),
+            'avg_call_ms': round(ms, 4), 'bytes_per_call': nbytes,
+            'basis': f'{B} utterances x ({4 * L} B samples in + {4 * 80 * nfr} B features out) per call, '
+                     'HIP events over back-to-back calls'}
+
+
 def physical_cores():
     """Physical cores of this host (lscpu: cores per socket x sockets), capped at the 16-CPU
     share a one-GPU box gives a job; os.cpu_count() counts SMT threads of the whole machine."""
@@ -230,6 +265,8 @@ def main():
             dt = float(t.item())
         feats = _hip.fbank(wavs, 80, mean_nor=True)
         roof = roofline(model, feats, device, args.traffic_json) if rank == 0 else None
+        if roof is not None:
+            roof['fbank'] = fbank_roofline(wavs, device)
 
     total_utts = B * args.steps * world
     value = total_utts / dt

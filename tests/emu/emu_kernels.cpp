@@ -180,7 +180,7 @@ hipError_t launch_tstp(const float* x, int B, int H, int W, int C, int ld, float
   return hipSuccess;
 }
 
-hipError_t launch_fbank(const float*, const int64_t*, int, float*, const int64_t*, int, int, const FbankTables*,
+hipError_t launch_fbank(const float*, const int64_t*, int, float*, const int64_t*, int, int, const FbankTables*, int,
                         hipStream_t, int) {
   return hipErrorNotSupported;
 }

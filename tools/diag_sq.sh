@@ -1,5 +1,6 @@
 #!/bin/bash
-# Diagnostics: SQ counter passes over one ERes2NetV2 forward (per-kernel ratios to SQ_WAVE_CYCLES).
+# Diagnostics: SQ counter passes over one ERes2NetV2 forward, or over SQ_CMD (a python script
+# and its arguments); per-kernel ratios to SQ_WAVE_CYCLES.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -12,7 +13,7 @@ for p in $P1 $P2 $P3; do
   i=$((i+1))
   echo "== pmc pass $i $(date +%T)"
   timeout -s KILL 120 rocprofv3 --pmc $p -d gpurun_out/sq$i -o run --output-format csv -- \
-      python tools/profile_steps.py --arch ${ARCH:-eres2netv2} > gpurun_out/sq$i.log 2>&1
+      python ${SQ_CMD:-tools/profile_steps.py --arch ${ARCH:-eres2netv2}} > gpurun_out/sq$i.log 2>&1
   rc=$?; echo "rc=$rc"; if [ $rc -ne 0 ]; then tail -5 gpurun_out/sq$i.log; exit $rc; fi
   python tools/pmc_sq.py gpurun_out/sq$i | head -8
 done
