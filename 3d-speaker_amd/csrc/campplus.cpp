@@ -13,10 +13,11 @@
 //     over the [B, F/8, T, 32] FCM output, with the weight re-indexed on the host;
 //   * a dense layer's BN-ReLU pre-activation is applied in the operand loader (pre_scale),
 //     its second BN-ReLU is folded into linear1's epilogue;
-//   * CAMLayer's context (mean + 100-frame segment means) is one reduction; its two 1x1
-//     layers run on B*nseg rows (the context is constant inside a segment, so this is the
-//     reference's per-frame computation without the repetition); the sigmoid gate
-//     multiplies linear_local's output in its epilogue;
+//   * CAMLayer's context branch (mean + 100-frame segment means -> linear1 -> ReLU ->
+//     linear2 -> sigmoid) is one kernel per utterance (cam_gate, tdnn_ops.hip): the context
+//     is constant inside a segment, so both 1x1 layers run once per segment -- the
+//     reference's per-frame computation without the repetition; the gate multiplies
+//     linear_local's output in its epilogue;
 //   * torch.cat growth is an in-place write into the block's preallocated channel buffer;
 //     transit layers write straight into the next block's buffer; out_nonlinear is folded
 //     into the last transit's epilogue; dense + BN(affine=False) is one small GEMM.
@@ -199,8 +200,6 @@ void build_campplus(Builder& b, int T) {
   const int bnc = (int)m.dim("xvector.block1.tdnnd1.linear1.weight", 0);   // bn_channels (128)
   const int red = (int)m.dim("xvector.block1.tdnnd1.cam_layer.linear1.weight", 0);
   const Buf Hh = b.alloc((size_t)B * T2 * bnc);
-  const Buf CTX = b.alloc((size_t)B * nseg * bnc);
-  const Buf CM = b.alloc((size_t)B * nseg * red);
   const Buf GATE = b.alloc((size_t)B * nseg * 64);
   Buf xo_final;
   int c_final = 0;
@@ -243,27 +242,18 @@ void build_campplus(Builder& b, int T) {
         b.macs_per_utt += m_l1;
         b.conv(q + ".linear1", d, l1, io);
       }
-      b.step(c + ".context", [=](const Ctx& cx) {
-        return launch_cam_context(cx.resolve(Hh), B, T2, bnc, bnc, 100, nseg, cx.resolve(CTX), bnc, cx.stream,
-                                  cx.resolve_i(LEN2));
-      });
       {
-        ConvDesc d;
-        d.nimg = B * nseg; d.Ho = 1; d.Wo = 1;
-        ConvSrc s; s.ld = bnc; s.cin = bnc;
-        d.s0 = s;
-        d.ldo = red; d.act = ACT_RELU;
-        Builder::ConvIO io; io.s0 = CTX; io.out = CM;
-        b.macs_per_utt += m_c1;
-        b.conv(c + ".linear1", d, cl1, io);
-        ConvDesc e;
-        e.nimg = B * nseg; e.Ho = 1; e.Wo = 1;
-        ConvSrc s2; s2.ld = red; s2.cin = red;
-        e.s0 = s2;
-        e.ldo = growth; e.act = ACT_SIGMOID;
-        Builder::ConvIO io2; io2.s0 = CM; io2.out = GATE;
-        b.macs_per_utt += m_c2;
-        b.conv(c + ".linear2", e, cl2, io2);
+        // context -> linear1 -> ReLU -> linear2 -> sigmoid, once per (utterance, segment)
+        const float* w1 = m.dptr(cl1.w_off);
+        const float* b1 = cl1.has_bias ? m.dptr(cl1.b_off) : nullptr;
+        const float* w2 = m.dptr(cl2.w_off);
+        const float* b2 = cl2.has_bias ? m.dptr(cl2.b_off) : nullptr;
+        const int k1p = cl1.Kp, k2p = cl2.Kp;
+        b.macs_per_utt += m_c1 + m_c2;
+        b.step(c + ".gate", [=](const Ctx& cx) {
+          return launch_cam_gate(cx.resolve(Hh), B, T2, bnc, bnc, 100, nseg, w1, k1p, b1, red, w2, k2p, b2, growth,
+                                 cx.resolve(GATE), growth, cx.stream, cx.resolve_i(LEN2));
+        }, "cam_gate_kernel", 4.0 * B * T2 * bnc);
       }
       {
         const A4 hh{Hh, bnc, 1, T2, bnc};

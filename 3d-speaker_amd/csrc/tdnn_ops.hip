@@ -15,6 +15,8 @@ namespace spk {
 
 namespace {
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 inline int grid_for(long long n) { return (int)std::min<long long>((n + 255) / 256, 65536); }
 
 // vlen (optional): utterance b's statistics cover frames [0, valid(b)) only -- ECAPA's
@@ -127,6 +129,81 @@ __global__ void cam_context_kernel(const float* __restrict__ x, int B, int T, in
   }
 }
 
+// CAMLayer's whole context branch (campplus/layers.py:93-110: context = mean_T(x) +
+// seg_pooling(x, 100) -> linear1 -> ReLU -> linear2 -> sigmoid) for one utterance per
+// workgroup.  The context is constant inside a 100-frame segment, so both 1x1 layers run
+// once per segment, in fp32 on the VALU (K = 128 / 64: far too small for MFMA tiles); the
+// gate [B][nseg][growth] then scales linear_local's output rows in its epilogue.  Rows as
+// float4 column quads x row lanes; sums in a fixed order (deterministic).
+__global__ void __launch_bounds__(256)
+cam_gate_kernel(const float* __restrict__ x, int T, int C, int ld, int seg, int nseg, const float* __restrict__ w1,
+                int k1p, const float* __restrict__ b1, int red, const float* __restrict__ w2, int k2p,
+                const float* __restrict__ b2, int growth, float* __restrict__ gate, int ldg,
+                const int* __restrict__ vlen) {
+  extern __shared__ float sm[];
+  const int nq = C / 4, RL = blockDim.x / nq;
+  float* part = sm;                  // [RL][C] row-lane partial sums, later dot partials
+  float* tot = part + RL * C;        // [C]
+  float* ctx = tot + C;              // [C]
+  float* h = ctx + C;                // [red]
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int Tb = valid_frames(vlen, b, T);
+  const int cq = tid % nq, rl = tid / nq;
+  const bool act = rl < RL;
+  const float* xb = x + (size_t)b * T * ld + cq * 4;
+  auto rows_sum = [&](int t0, int t1, float* dst) {   // dst[c] = sum_{t0 <= t < t1} x[t][c]
+    f32x4 a = {0.f, 0.f, 0.f, 0.f};
+    if (act) {
+      int t = t0 + rl;
+      for (; t + 3 * RL < t1; t += 4 * RL) {    // four independent row loads in flight
+        const f32x4 q0 = *reinterpret_cast<const f32x4*>(xb + (size_t)t * ld);
+        const f32x4 q1 = *reinterpret_cast<const f32x4*>(xb + (size_t)(t + RL) * ld);
+        const f32x4 q2 = *reinterpret_cast<const f32x4*>(xb + (size_t)(t + 2 * RL) * ld);
+        const f32x4 q3 = *reinterpret_cast<const f32x4*>(xb + (size_t)(t + 3 * RL) * ld);
+        a += q0; a += q1; a += q2; a += q3;
+      }
+      for (; t < t1; t += RL) a += *reinterpret_cast<const f32x4*>(xb + (size_t)t * ld);
+      *reinterpret_cast<f32x4*>(part + rl * C + cq * 4) = a;
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += blockDim.x) {
+      float v = 0.f;
+      for (int r = 0; r < RL; ++r) v += part[r * C + c];
+      dst[c] = v;
+    }
+    __syncthreads();
+  };
+  // out[n] = act(bias[n] + sum_k w[n * kp + k] in[k]) for n < N: P = blockDim / N partial
+  // dots per output over contiguous K slices, combined in slice order
+  auto dense = [&](const float* in, int K, const float* w, int kp, const float* bias, int N, bool relu, float* out) {
+    const int P = blockDim.x / N, n = tid % N, pi = tid / N, kk = (K + P - 1) / P;
+    if (pi < P) {
+      const int k0 = pi * kk, k1 = min(K, k0 + kk);
+      const float* wr = w + (size_t)n * kp;
+      float a = 0.f;
+      for (int k = k0; k < k1; ++k) a += wr[k] * in[k];
+      part[pi * N + n] = a;
+    }
+    __syncthreads();
+    if (tid < N) {
+      float v = bias ? bias[tid] : 0.f;
+      for (int q = 0; q < P; ++q) v += part[q * N + tid];
+      out[tid] = relu ? fmaxf(v, 0.f) : 1.0f / (1.0f + __expf(-v));
+    }
+    __syncthreads();
+  };
+  rows_sum(0, Tb, tot);
+  for (int sg = 0; sg < nseg; ++sg) {
+    const int t0 = sg * seg, t1 = min(Tb, t0 + seg);
+    rows_sum(t0, max(t0, t1), ctx);
+    for (int c = tid; c < C; c += blockDim.x)
+      ctx[c] = t1 > t0 ? tot[c] / (float)Tb + ctx[c] / (float)(t1 - t0) : 0.f;
+    __syncthreads();
+    dense(ctx, C, w1, k1p, b1, red, true, h);
+    dense(h, red, w2, k2p, b2, growth, false, gate + ((size_t)b * nseg + sg) * ldg);
+  }
+}
+
 __global__ void stats_pool_kernel(const float* __restrict__ x, int B, int T, int C, int ld, float* __restrict__ out,
                                   const int* __restrict__ vlen) {
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
@@ -187,6 +264,19 @@ hipError_t launch_cam_context(const float* x, int B, int T, int C, int ld, int s
                               hipStream_t s, const int* vlen) {
   hipLaunchKernelGGL(cam_context_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, seg, nseg,
                      out, ldo, vlen);
+  return hipGetLastError();
+}
+
+hipError_t launch_cam_gate(const float* x, int B, int T, int C, int ld, int seg, int nseg, const float* w1, int k1p,
+                          const float* b1, int red, const float* w2, int k2p, const float* b2, int growth, float* gate,
+                          int ldg, hipStream_t s, const int* vlen) {
+  if (C % 4 || C / 4 > 256 || ld % 4 || red <= 0 || red > 256 || growth <= 0 || growth > 256 || B <= 0 || nseg <= 0)
+    return hipErrorInvalidValue;
+  const int RL = 256 / (C / 4);
+  const size_t lds = sizeof(float) * ((size_t)RL * C + 2 * C + red);
+  if ((size_t)256 > (size_t)RL * C) return hipErrorInvalidValue;   // dot partials reuse the row-lane block
+  hipLaunchKernelGGL(cam_gate_kernel, dim3(B), dim3(256), lds, s, x, T, C, ld, seg, nseg, w1, k1p, b1, red, w2, k2p,
+                     b2, growth, gate, ldg, vlen);
   return hipGetLastError();
 }
 

@@ -366,6 +366,34 @@ hipError_t launch_se_apply(const float* x, int ldx, const float* g, int ldg, con
       }
   return hipSuccess;
 }
+hipError_t launch_cam_gate(const float* x, int B, int T, int C, int ld, int seg, int nseg, const float* w1, int k1p,
+                          const float* b1, int red, const float* w2, int k2p, const float* b2, int growth, float* gate,
+                          int ldg, hipStream_t, const int* vlen) {
+  std::vector<double> ctx(C), h(red);
+  for (int b = 0; b < B; ++b) {
+    const int Tb = vlen ? std::min(std::max(vlen[b], 1), T) : T;
+    for (int s = 0; s < nseg; ++s) {
+      const int t0 = s * seg, t1 = std::min(Tb, t0 + seg);
+      for (int c = 0; c < C; ++c) {
+        double tot = 0, a = 0;
+        for (int t = 0; t < Tb; ++t) tot += x[((size_t)b * T + t) * ld + c];
+        for (int t = t0; t < t1; ++t) a += x[((size_t)b * T + t) * ld + c];
+        ctx[c] = t1 > t0 ? tot / Tb + a / (t1 - t0) : 0.0;
+      }
+      for (int j = 0; j < red; ++j) {
+        double v = b1 ? b1[j] : 0.0;
+        for (int c = 0; c < C; ++c) v += (double)w1[(size_t)j * k1p + c] * ctx[c];
+        h[j] = std::max(v, 0.0);
+      }
+      for (int i = 0; i < growth; ++i) {
+        double v = b2 ? b2[i] : 0.0;
+        for (int j = 0; j < red; ++j) v += (double)w2[(size_t)i * k2p + j] * h[j];
+        gate[((size_t)b * nseg + s) * ldg + i] = (float)(1.0 / (1.0 + std::exp(-v)));
+      }
+    }
+  }
+  return hipSuccess;
+}
 hipError_t launch_cam_context(const float* x, int B, int T, int C, int ld, int seg, int nseg, float* out, int ldo,
                               hipStream_t, const int* vlen) {
   for (int b = 0; b < B; ++b) {
