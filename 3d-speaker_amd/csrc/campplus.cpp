@@ -201,6 +201,7 @@ void build_campplus(Builder& b, int T) {
   const int red = (int)m.dim("xvector.block1.tdnnd1.cam_layer.linear1.weight", 0);
   const Buf Hh = b.alloc((size_t)B * T2 * bnc);
   const Buf GATE = b.alloc((size_t)B * nseg * 64);
+  const Buf SEGSUM = b.alloc((size_t)B * nseg * bnc);
   Buf xo_final;
   int c_final = 0;
   for (size_t bi = 0; bi < blks.size(); ++bi) {
@@ -252,7 +253,7 @@ void build_campplus(Builder& b, int T) {
         b.macs_per_utt += m_c1 + m_c2;
         b.step(c + ".gate", [=](const Ctx& cx) {
           return launch_cam_gate(cx.resolve(Hh), B, T2, bnc, bnc, 100, nseg, w1, k1p, b1, red, w2, k2p, b2, growth,
-                                 cx.resolve(GATE), growth, cx.stream, cx.resolve_i(LEN2));
+                                 cx.resolve(GATE), growth, cx.resolve(SEGSUM), cx.stream, cx.resolve_i(LEN2));
         }, "cam_gate_kernel", 4.0 * B * T2 * bnc);
       }
       {

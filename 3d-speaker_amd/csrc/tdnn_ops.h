@@ -17,10 +17,11 @@ hipError_t launch_se_apply(const float* x, int ldx, const float* gate, int ldg, 
 hipError_t launch_cam_context(const float* x, int B, int T, int C, int ld, int seg, int nseg, float* out, int ldo,
                               hipStream_t s, const int* vlen = nullptr);
 // CAMLayer context -> linear1 -> ReLU -> linear2 -> sigmoid, once per (utterance, segment):
-// gate[(b * nseg + s) * ldg + i]; w1 [red][k1p], w2 [growth][k2p] fp32 (packed GEMM weights)
+// gate[(b * nseg + s) * ldg + i]; w1 [red][k1p], w2 [growth][k2p] fp32 (packed GEMM weights);
+// segsum: [B][nseg][C] floats of scratch
 hipError_t launch_cam_gate(const float* x, int B, int T, int C, int ld, int seg, int nseg, const float* w1, int k1p,
                           const float* b1, int red, const float* w2, int k2p, const float* b2, int growth, float* gate,
-                          int ldg, hipStream_t s, const int* vlen = nullptr);
+                          int ldg, float* segsum, hipStream_t s, const int* vlen = nullptr);
 hipError_t launch_stats_pool(const float* x, int B, int T, int C, int ld, float* out, hipStream_t s,
                              const int* vlen = nullptr);
 // out[b] = (in[b] + 2 pad - k) / stride + 1 (valid frames after a strided conv)

@@ -16,6 +16,7 @@ namespace spk {
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int CAM_SEGS = 4;   // segments whose 1x1 layers run together (weights read once)
 
 inline int grid_for(long long n) { return (int)std::min<long long>((n + 255) / 256, 65536); }
 
@@ -129,78 +130,116 @@ __global__ void cam_context_kernel(const float* __restrict__ x, int B, int T, in
   }
 }
 
-// CAMLayer's whole context branch (campplus/layers.py:93-110: context = mean_T(x) +
-// seg_pooling(x, 100) -> linear1 -> ReLU -> linear2 -> sigmoid) for one utterance per
-// workgroup.  The context is constant inside a 100-frame segment, so both 1x1 layers run
-// once per segment, in fp32 on the VALU (K = 128 / 64: far too small for MFMA tiles); the
-// gate [B][nseg][growth] then scales linear_local's output rows in its epilogue.  Rows as
-// float4 column quads x row lanes; sums in a fixed order (deterministic).
+// CAMLayer's context branch (campplus/layers.py:93-110: context = mean_T(x) +
+// seg_pooling(x, 100) -> linear1 -> ReLU -> linear2 -> sigmoid).  The context is constant
+// inside a 100-frame segment, so both 1x1 layers run once per segment, in fp32 on the
+// VALU (K = 128 / 64: far too small for MFMA tiles); the gate [B][nseg][growth] then
+// scales linear_local's output rows in its epilogue.  Two kernels:
+//  * cam_segsum: one workgroup per (segment, utterance) sums the segment's valid rows
+//    (float4 column quads x row lanes, four row loads in flight, fixed-order reduction);
+//  * cam_gate: one workgroup per utterance: mean = (sum of its segment sums) / T, the
+//    contexts, and both layers with the weights staged transposed in LDS.
 __global__ void __launch_bounds__(256)
-cam_gate_kernel(const float* __restrict__ x, int T, int C, int ld, int seg, int nseg, const float* __restrict__ w1,
+cam_segsum_kernel(const float* __restrict__ x, int T, int C, int ld, int seg, int nseg, float* __restrict__ segsum,
+                  const int* __restrict__ vlen) {
+  __shared__ f32x4 part[256];
+  const int sg = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int Tb = valid_frames(vlen, b, T);
+  const int nq = C / 4, RL = blockDim.x / nq;
+  const int cq = tid % nq, rl = tid / nq;
+  const int t0 = sg * seg, t1 = min(Tb, t0 + seg);
+  f32x4 a = {0.f, 0.f, 0.f, 0.f};
+  if (rl < RL) {
+    const float* xb = x + (size_t)b * T * ld + cq * 4;
+    int t = t0 + rl;
+    for (; t + 3 * RL < t1; t += 4 * RL) {
+      const f32x4 q0 = *reinterpret_cast<const f32x4*>(xb + (size_t)t * ld);
+      const f32x4 q1 = *reinterpret_cast<const f32x4*>(xb + (size_t)(t + RL) * ld);
+      const f32x4 q2 = *reinterpret_cast<const f32x4*>(xb + (size_t)(t + 2 * RL) * ld);
+      const f32x4 q3 = *reinterpret_cast<const f32x4*>(xb + (size_t)(t + 3 * RL) * ld);
+      a += q0; a += q1; a += q2; a += q3;
+    }
+    for (; t < t1; t += RL) a += *reinterpret_cast<const f32x4*>(xb + (size_t)t * ld);
+  }
+  part[tid] = a;
+  __syncthreads();
+  if (tid < nq) {
+    f32x4 v = part[tid];
+    for (int r = 1; r < RL; ++r) v += part[r * nq + tid];
+    *reinterpret_cast<f32x4*>(segsum + ((size_t)b * nseg + sg) * C + tid * 4) = v;
+  }
+}
+
+__global__ void __launch_bounds__(1024)
+cam_gate_kernel(const float* __restrict__ segsum, int T, int C, int seg, int nseg, const float* __restrict__ w1,
                 int k1p, const float* __restrict__ b1, int red, const float* __restrict__ w2, int k2p,
                 const float* __restrict__ b2, int growth, float* __restrict__ gate, int ldg,
                 const int* __restrict__ vlen) {
   extern __shared__ float sm[];
-  const int nq = C / 4, RL = blockDim.x / nq;
-  float* part = sm;                  // [RL][C] row-lane partial sums, later dot partials
-  float* tot = part + RL * C;        // [C]
-  float* ctx = tot + C;              // [C]
-  float* h = ctx + C;                // [red]
+  float* w1t = sm;                          // [C][red + 1]  (transposed, padded: conflict-free)
+  float* w2t = w1t + C * (red + 1);         // [red][growth + 1]
+  float* mean = w2t + red * (growth + 1);   // [C]
+  float* ctx = mean + C;                    // [CAM_SEGS][C]
+  float* h = ctx + CAM_SEGS * C;            // [CAM_SEGS][red]
+  float* part = h + CAM_SEGS * red;         // [CAM_SEGS][1024] dot partials
   const int b = blockIdx.x, tid = threadIdx.x;
   const int Tb = valid_frames(vlen, b, T);
-  const int cq = tid % nq, rl = tid / nq;
-  const bool act = rl < RL;
-  const float* xb = x + (size_t)b * T * ld + cq * 4;
-  auto rows_sum = [&](int t0, int t1, float* dst) {   // dst[c] = sum_{t0 <= t < t1} x[t][c]
-    f32x4 a = {0.f, 0.f, 0.f, 0.f};
-    if (act) {
-      int t = t0 + rl;
-      for (; t + 3 * RL < t1; t += 4 * RL) {    // four independent row loads in flight
-        const f32x4 q0 = *reinterpret_cast<const f32x4*>(xb + (size_t)t * ld);
-        const f32x4 q1 = *reinterpret_cast<const f32x4*>(xb + (size_t)(t + RL) * ld);
-        const f32x4 q2 = *reinterpret_cast<const f32x4*>(xb + (size_t)(t + 2 * RL) * ld);
-        const f32x4 q3 = *reinterpret_cast<const f32x4*>(xb + (size_t)(t + 3 * RL) * ld);
-        a += q0; a += q1; a += q2; a += q3;
-      }
-      for (; t < t1; t += RL) a += *reinterpret_cast<const f32x4*>(xb + (size_t)t * ld);
-      *reinterpret_cast<f32x4*>(part + rl * C + cq * 4) = a;
-    }
-    __syncthreads();
-    for (int c = tid; c < C; c += blockDim.x) {
-      float v = 0.f;
-      for (int r = 0; r < RL; ++r) v += part[r * C + c];
-      dst[c] = v;
-    }
-    __syncthreads();
-  };
-  // out[n] = act(bias[n] + sum_k w[n * kp + k] in[k]) for n < N: P = blockDim / N partial
-  // dots per output over contiguous K slices, combined in slice order
-  auto dense = [&](const float* in, int K, const float* w, int kp, const float* bias, int N, bool relu, float* out) {
+#pragma unroll 4
+  for (int e = tid; e < red * C; e += blockDim.x) {       // coalesced rows, transposed into LDS
+    const int n = e / C, k = e - n * C;
+    w1t[k * (red + 1) + n] = w1[(size_t)n * k1p + k];
+  }
+#pragma unroll 2
+  for (int e = tid; e < growth * red; e += blockDim.x) {
+    const int n = e / red, k = e - n * red;
+    w2t[k * (growth + 1) + n] = w2[(size_t)n * k2p + k];
+  }
+  const float* ss = segsum + (size_t)b * nseg * C;
+  for (int c = tid; c < C; c += blockDim.x) {
+    float v = 0.f;
+    for (int sg = 0; sg < nseg; ++sg) v += ss[(size_t)sg * C + c];
+    mean[c] = v / (float)Tb;
+  }
+  __syncthreads();
+  // out[s][n] = act(bias[n] + sum_k wt[k][n] in[s][k]): P = blockDim / N partial dots per
+  // output over contiguous K slices (all segments of the chunk at once), then in slice order
+  auto dense = [&](const float* in, int K, const float* wt, int N, const float* bias, bool relu, int ns, float* out,
+                   int ldout) {
     const int P = blockDim.x / N, n = tid % N, pi = tid / N, kk = (K + P - 1) / P;
     if (pi < P) {
+      float acc[CAM_SEGS];
+#pragma unroll
+      for (int j = 0; j < CAM_SEGS; ++j) acc[j] = 0.f;
       const int k0 = pi * kk, k1 = min(K, k0 + kk);
-      const float* wr = w + (size_t)n * kp;
-      float a = 0.f;
-      for (int k = k0; k < k1; ++k) a += wr[k] * in[k];
-      part[pi * N + n] = a;
+      for (int k = k0; k < k1; ++k) {
+        const float wv = wt[k * (N + 1) + n];
+#pragma unroll
+        for (int j = 0; j < CAM_SEGS; ++j)
+          if (j < ns) acc[j] += wv * in[j * K + k];
+      }
+#pragma unroll
+      for (int j = 0; j < CAM_SEGS; ++j)
+        if (j < ns) part[j * 1024 + pi * N + n] = acc[j];
     }
     __syncthreads();
-    if (tid < N) {
-      float v = bias ? bias[tid] : 0.f;
-      for (int q = 0; q < P; ++q) v += part[q * N + tid];
-      out[tid] = relu ? fmaxf(v, 0.f) : 1.0f / (1.0f + __expf(-v));
+    for (int e = tid; e < ns * N; e += blockDim.x) {
+      const int j = e / N, o = e - j * N;
+      float v = bias ? bias[o] : 0.f;
+      for (int q = 0; q < P; ++q) v += part[j * 1024 + q * N + o];
+      out[(size_t)j * ldout + o] = relu ? fmaxf(v, 0.f) : 1.0f / (1.0f + __expf(-v));
     }
     __syncthreads();
   };
-  rows_sum(0, Tb, tot);
-  for (int sg = 0; sg < nseg; ++sg) {
-    const int t0 = sg * seg, t1 = min(Tb, t0 + seg);
-    rows_sum(t0, max(t0, t1), ctx);
-    for (int c = tid; c < C; c += blockDim.x)
-      ctx[c] = t1 > t0 ? tot[c] / (float)Tb + ctx[c] / (float)(t1 - t0) : 0.f;
+  for (int s0 = 0; s0 < nseg; s0 += CAM_SEGS) {
+    const int ns = min(CAM_SEGS, nseg - s0);
+    for (int e = tid; e < ns * C; e += blockDim.x) {
+      const int j = e / C, c = e - j * C;
+      const int t0 = (s0 + j) * seg, t1 = min(Tb, t0 + seg);
+      ctx[e] = t1 > t0 ? mean[c] + ss[(size_t)(s0 + j) * C + c] / (float)(t1 - t0) : 0.f;
+    }
     __syncthreads();
-    dense(ctx, C, w1, k1p, b1, red, true, h);
-    dense(h, red, w2, k2p, b2, growth, false, gate + ((size_t)b * nseg + sg) * ldg);
+    dense(ctx, C, w1t, red, b1, true, ns, h, red);
+    dense(h, red, w2t, growth, b2, false, ns, gate + ((size_t)b * nseg + s0) * ldg, ldg);
   }
 }
 
@@ -269,13 +308,15 @@ hipError_t launch_cam_context(const float* x, int B, int T, int C, int ld, int s
 
 hipError_t launch_cam_gate(const float* x, int B, int T, int C, int ld, int seg, int nseg, const float* w1, int k1p,
                           const float* b1, int red, const float* w2, int k2p, const float* b2, int growth, float* gate,
-                          int ldg, hipStream_t s, const int* vlen) {
-  if (C % 4 || C / 4 > 256 || ld % 4 || red <= 0 || red > 256 || growth <= 0 || growth > 256 || B <= 0 || nseg <= 0)
+                          int ldg, float* segsum, hipStream_t s, const int* vlen) {
+  if (C % 4 || C / 4 > 256 || ld % 4 || red <= 0 || red > 1024 || growth <= 0 || growth > 1024 || B <= 0 || nseg <= 0)
     return hipErrorInvalidValue;
-  const int RL = 256 / (C / 4);
-  const size_t lds = sizeof(float) * ((size_t)RL * C + 2 * C + red);
-  if ((size_t)256 > (size_t)RL * C) return hipErrorInvalidValue;   // dot partials reuse the row-lane block
-  hipLaunchKernelGGL(cam_gate_kernel, dim3(B), dim3(256), lds, s, x, T, C, ld, seg, nseg, w1, k1p, b1, red, w2, k2p,
+  hipLaunchKernelGGL(cam_segsum_kernel, dim3(nseg, B), dim3(256), 0, s, x, T, C, ld, seg, nseg, segsum, vlen);
+  if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  const size_t lds = sizeof(float) * ((size_t)C * (red + 1) + (size_t)red * (growth + 1) + C +
+                                      CAM_SEGS * (C + red + 1024));
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(cam_gate_kernel, dim3(B), dim3(1024), lds, s, segsum, T, C, seg, nseg, w1, k1p, b1, red, w2, k2p,
                      b2, growth, gate, ldg, vlen);
   return hipGetLastError();
 }

@@ -368,7 +368,7 @@ hipError_t launch_se_apply(const float* x, int ldx, const float* g, int ldg, con
 }
 hipError_t launch_cam_gate(const float* x, int B, int T, int C, int ld, int seg, int nseg, const float* w1, int k1p,
                           const float* b1, int red, const float* w2, int k2p, const float* b2, int growth, float* gate,
-                          int ldg, hipStream_t, const int* vlen) {
+                          int ldg, float*, hipStream_t, const int* vlen) {
   std::vector<double> ctx(C), h(red);
   for (int b = 0; b < B; ++b) {
     const int Tb = vlen ? std::min(std::max(vlen[b], 1), T) : T;
