@@ -44,6 +44,9 @@ ConvSrc src2d(const A4& t, int cin, int kh, int kw, int sh, int sw, int ph, int 
 }  // namespace
 
 void build_campplus(Builder& b, int T) {
+  // reduced-precision mode: only the dense blocks' GEMMs (the bulk of the FLOPs) run as single
+  // products; the FCM head, the TDNN layer, transits and the embedding layer stay fp16x3
+  b.x1_scope = false;
   Model& m = b.m;
   const int B = b.B;
   const int F = m.cfg.feat_dim;
@@ -206,6 +209,7 @@ void build_campplus(Builder& b, int T) {
   int c_final = 0;
   for (size_t bi = 0; bi < blks.size(); ++bi) {
     const Blk& bk = blks[bi];
+    b.x1_scope = true;
     const std::string p = "xvector.block" + std::to_string(bi + 1);
     for (int l = 0; l < bk.n; ++l) {
       const std::string q = p + ".tdnnd" + std::to_string(l + 1);
@@ -268,6 +272,7 @@ void build_campplus(Builder& b, int T) {
         b.conv(c + ".linear_local", d, loc, io);
       }
     }
+    b.x1_scope = false;
     // transit: BN-ReLU (pre) -> 1x1 (no bias); the last one also folds out_nonlinear
     const std::string t = "xvector.transit" + std::to_string(bi + 1);
     const int cout = (int)m.dim(t + ".linear.weight", 0);

@@ -66,6 +66,7 @@ struct ConvDesc {
   int ksplit = 1; float* partial = nullptr;            // split-K partial slabs [ksplit][M][N]
   const int* rowlen = nullptr;  // ragged batches: outputs with wo >= rowlen[img] are written as 0
   int* range_flag = nullptr;    // fp16x3 range guard (below): set when an output reaches kRangeLimit
+  int x1 = 0;                   // single-product fp16 MFMA (SPK_PRECISION_FP16): hi planes only
 };
 
 // fp16x3 range guard.  The split-precision GEMMs represent an operand as two fp16 values,

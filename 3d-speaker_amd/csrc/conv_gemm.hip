@@ -175,23 +175,27 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool X1 = false>
 struct X3Cfg {
   static constexpr int BK = 32, NT = 64 * WM * WN;
   static constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32;
   static constexpr int QPR = BK / 4, RPP = NT / QPR, AROWS = BM / RPP;             // A: fp32 quads
-  static constexpr int CPR = 8, RPPB = NT / CPR, BROWS = (BN + RPPB - 1) / RPPB;   // B: 16-B chunks
+  // B: 16-B chunks, four per 32-half row and plane; x3 spreads the block over both planes
+  static constexpr int CPR = X1 ? 4 : 8, RPPB = NT / CPR, BROWS = (BN + RPPB - 1) / RPPB;
   static constexpr int LROW = BK + 8;                                               // halves
   static constexpr int PA = BM * LROW, PB = BN * LROW;
-  static constexpr int STAGE = 2 * PA + 2 * PB;       // halves per buffer = floats for both buffers
+  static constexpr int NPL = X1 ? 1 : 2;               // planes per operand (hi, lo)
+  static constexpr int STAGE = NPL * (PA + PB);        // halves per buffer = floats for both buffers
   static constexpr int LDS_EPI = WM * WN * TM * TN * 1024;
   static constexpr int LDS_FLOATS = STAGE > LDS_EPI ? STAGE : LDS_EPI;
 };
 
-template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE, bool BUF>
-__global__ void __launch_bounds__(64 * WM * WN, (BM * BN <= 128 * 128) ? 4 : 1)
-conv_gemm_x3_kernel(const ConvDesc d) {
-  using C = X3Cfg<BM, BN, WM, WN>;
+// X1 = the single-product variant (C3's reduced-precision mode, spk_model_config_t
+// precision = SPK_PRECISION_FP16): operands rounded to fp16 (round to nearest), one MFMA
+// per product, fp32 accumulation; only the hi planes are staged.
+template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE, bool BUF, bool X1>
+__device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
+  using C = X3Cfg<BM, BN, WM, WN, X1>;
   constexpr int BK = C::BK, TM = C::TM, TN = C::TN, RPP = C::RPP, AROWS = C::AROWS;
   static_assert(TM >= 1 && TN >= 1 && BM % RPP == 0, "tile shape");
   __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
@@ -222,8 +226,8 @@ conv_gemm_x3_kernel(const ConvDesc d) {
   // ---- B chunk geometry: the first half of the block loads the hi plane, the second the
   // lo plane (wave-uniform, so each wave reads through one buffer resource); a thread owns
   // one 16-B quarter of a 32-half weight row.  Rows past N read zeros (offset past range).
-  const int plane = __builtin_amdgcn_readfirstlane(tid / (C::NT / 2));
-  const int bq = tid & 3, brow0 = (tid % (C::NT / 2)) >> 2;
+  const int plane = X1 ? 0 : __builtin_amdgcn_readfirstlane(tid / (C::NT / 2));
+  const int bq = tid & 3, brow0 = X1 ? tid >> 2 : (tid % (C::NT / 2)) >> 2;
   const __amdgpu_buffer_rsrc_t brs = make_rsrc(plane ? d.wl : d.wh);
   uint32_t boff[C::BROWS];
 #pragma unroll
@@ -250,17 +254,21 @@ conv_gemm_x3_kernel(const ConvDesc d) {
   auto store_tile = [&](int buf, const Set& st) {
     _Float16* ahi = hl + buf * C::STAGE;
     _Float16* alo = ahi + C::PA;
-    _Float16* bpl = ahi + 2 * C::PA + plane * C::PB;
+    _Float16* bpl = ahi + C::NPL * C::PA + plane * C::PB;
 #pragma unroll
     for (int r = 0; r < AROWS; ++r) {
       const f32x4 v = al.value(st.a, r);
       // packed round-toward-zero split (conv_epilogue.h split_x3; measured -0.3 ms per
       // ERes2NetV2 forward against per-element round-to-nearest conversions)
-      f16x4 h, l;
-      split_x3(v, h, l);
       const int off = (row0 + RPP * r) * C::LROW + kq * 4;
-      *reinterpret_cast<f16x4*>(ahi + off) = h;
-      *reinterpret_cast<f16x4*>(alo + off) = l;
+      if constexpr (X1) {
+        *reinterpret_cast<f16x4*>(ahi + off) = __builtin_convertvector(v, f16x4);
+      } else {
+        f16x4 h, l;
+        split_x3(v, h, l);
+        *reinterpret_cast<f16x4*>(ahi + off) = h;
+        *reinterpret_cast<f16x4*>(alo + off) = l;
+      }
     }
 #pragma unroll
     for (int r = 0; r < C::BROWS; ++r) {
@@ -280,7 +288,7 @@ conv_gemm_x3_kernel(const ConvDesc d) {
   const int li = lane & 31, lh = lane >> 5;
   auto compute = [&](int buf) {
     const _Float16* ahi = hl + buf * C::STAGE;
-    const _Float16* bhi = ahi + 2 * C::PA;
+    const _Float16* bhi = ahi + C::NPL * C::PA;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       f16x8 ah[TM], al[TM], bh[TN], bl[TN];
@@ -288,21 +296,23 @@ conv_gemm_x3_kernel(const ConvDesc d) {
       for (int i = 0; i < TM; ++i) {
         const _Float16* p = ahi + (wm * C::WTM + i * 32 + li) * C::LROW + lh * 16 + 8 * s;
         ah[i] = *reinterpret_cast<const f16x8*>(p);
-        al[i] = *reinterpret_cast<const f16x8*>(p + C::PA);
+        if constexpr (!X1) al[i] = *reinterpret_cast<const f16x8*>(p + C::PA);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const _Float16* p = bhi + (wn * C::WTN + j * 32 + li) * C::LROW + lh * 16 + 8 * s;
         bh[j] = *reinterpret_cast<const f16x8*>(p);
-        bl[j] = *reinterpret_cast<const f16x8*>(p + C::PB);
+        if constexpr (!X1) bl[j] = *reinterpret_cast<const f16x8*>(p + C::PB);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-          accx[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], accx[i][j], 0, 0, 0);
-          accx[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], accx[i][j], 0, 0, 0);
+          if constexpr (!X1) {
+            accx[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], accx[i][j], 0, 0, 0);
+            accx[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], accx[i][j], 0, 0, 0);
+          }
         }
     }
   };
@@ -333,11 +343,25 @@ conv_gemm_x3_kernel(const ConvDesc d) {
       __syncthreads();
     }
   }
+  if constexpr (!X1) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] += accx[i][j] * (1.0f / 2048.0f);
+      for (int j = 0; j < TN; ++j) acc[i][j] += accx[i][j] * (1.0f / 2048.0f);
+  }
   epilogue_tiles<TM, TN>(d, lds, acc, wave, lane, n0 + wn * C::WTN, M, [&](int r) { return m0 + wm * C::WTM + r; });
+}
+
+template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE, bool BUF>
+__global__ void __launch_bounds__(64 * WM * WN, (BM * BN <= 128 * 128) ? 4 : 1)
+conv_gemm_x3_kernel(const ConvDesc d) {
+  conv_gemm_f16_body<BM, BN, WM, WN, S1, ADD, PRE, BUF, false>(d);
+}
+
+template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE>
+__global__ void __launch_bounds__(64 * WM * WN, (BM * BN <= 128 * 128) ? 2 : 1)
+conv_gemm_x1_kernel(const ConvDesc d) {
+  conv_gemm_f16_body<BM, BN, WM, WN, S1, ADD, PRE, true, true>(d);
 }
 
 // Split-K combine: out = epi(sum_z partial[z])   (fixed z order: deterministic)
@@ -417,7 +441,12 @@ hipError_t launch_cfg(const ConvDesc& d, hipStream_t s) {
   dim3 block(64 * WM * WN);
   const bool s1 = d.s1.p != nullptr, add = d.s0.p2 != nullptr, pre = d.s0.pre_scale != nullptr;
   if ((int)s1 + (int)add + (int)pre > 1) return hipErrorInvalidValue;
-  if (use_x3() && d.wh && d.wl) {
+  if (d.x1 && d.wh && conv_buf_loader_ok(d, BM)) {
+    if (s1) hipLaunchKernelGGL((conv_gemm_x1_kernel<BM, BN, WM, WN, true, false, false>), grid, block, 0, s, d);
+    else if (add) hipLaunchKernelGGL((conv_gemm_x1_kernel<BM, BN, WM, WN, false, true, false>), grid, block, 0, s, d);
+    else if (pre) hipLaunchKernelGGL((conv_gemm_x1_kernel<BM, BN, WM, WN, false, false, true>), grid, block, 0, s, d);
+    else hipLaunchKernelGGL((conv_gemm_x1_kernel<BM, BN, WM, WN, false, false, false>), grid, block, 0, s, d);
+  } else if (use_x3() && d.wh && d.wl) {
     if (conv_buf_loader_ok(d, BM)) {
       if (s1) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, true, false, false, true>), grid, block, 0, s, d);
       else if (add) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, true, false, true>), grid, block, 0, s, d);
@@ -463,6 +492,8 @@ std::string conv_kernel_name(const ConvDesc& d) {
   const bool pre = d.s0.pre_scale != nullptr;
   const std::string tail = std::to_string(c.wm) + ", " + std::to_string(c.wn) + ", " + (s1 ? "true" : "false") + ", " +
                            (add ? "true" : "false") + ", " + (pre ? "true" : "false") + ">";
+  if (d.x1 && d.wh && conv_buf_loader_ok(d, c.bm))
+    return "conv_gemm_x1_kernel<" + std::to_string(c.bm) + ", " + std::to_string(c.bn) + ", " + tail;
   if (use_x3() && d.wh && d.wl)
     return "conv_gemm_x3_kernel<" + std::to_string(c.bm) + ", " + std::to_string(c.bn) + ", " +
            tail.substr(0, tail.size() - 1) + (conv_buf_loader_ok(d, c.bm) ? ", true>" : ", false>");

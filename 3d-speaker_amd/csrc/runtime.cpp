@@ -165,6 +165,7 @@ void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const C
   d.wh = exact ? nullptr : m.dhi(p.w_off);   // no split planes: the exact-fp32 kernels are chosen
   d.wl = exact ? nullptr : m.dlo(p.w_off);
   d.range_flag = exact ? nullptr : m.range_flag;
+  d.x1 = (!exact && m.fp16 && x1_scope) ? 1 : 0;
   d.bias = (use_bias && p.has_bias) ? m.dptr(p.b_off) : nullptr;
   const int M = d.nimg * d.Ho * d.Wo;
   // split-K for skinny, deep GEMMs (e.g. the 20480 -> 192 embedding layer)
@@ -371,8 +372,13 @@ int spk_model_create(const spk_model_config_t* cfg, const spk_weight_t* weights,
       set_error("spk_model_create: null argument");
       return SPK_E_INVALID;
     }
+    if (cfg->precision != SPK_PRECISION_FP32 && cfg->precision != SPK_PRECISION_FP16) {
+      set_error("spk_model_create: precision must be SPK_PRECISION_FP32 or SPK_PRECISION_FP16");
+      return SPK_E_INVALID;
+    }
     auto h = std::make_unique<spk_model>();
     h->m.cfg = *cfg;
+    h->m.fp16 = cfg->precision == SPK_PRECISION_FP16;
     if (int rc = hip_check(hipGetDevice(&h->m.device), "hipGetDevice")) return rc;
     for (int i = 0; i < n_weights; ++i) {
       const spk_weight_t& w = weights[i];

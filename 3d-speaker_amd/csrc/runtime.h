@@ -113,6 +113,7 @@ struct Model {
   static constexpr size_t kMaxPlans = 24;
   int* range_flag = nullptr;                      // device word of the fp16x3 range guard (common.h)
   bool force_exact = false;                       // a packed weight is out of fp16 range: exact path only
+  bool fp16 = false;                              // SPK_PRECISION_FP16: single-product fp16 GEMMs
   float gemm_wmax = 0.f;                          // max |w| over the packed GEMM weights
   std::mutex mu;
   bool uploaded = false;
@@ -143,6 +144,9 @@ struct Builder {
   double macs_at_last_step = 0;
   bool ragged = false;       // per-utterance lengths (Buf::LEN) mask the time axis
   bool exact = false;        // exact-fp32 MFMA kernels only (no fp16x3 split anywhere)
+  bool x1_scope = true;      // SPK_PRECISION_FP16 handles: convs emitted while set use the
+                             // single-product kernels (model builders keep the input-side
+                             // layers, whose error the network amplifies most, fp16x3)
   Builder(Model& mm, Plan* p, int b, bool rg = false, bool ex = false) : m(mm), plan(p), B(b), ragged(rg), exact(ex) {}
   bool x3() const { return !exact && conv_use_x3(); }
   Buf alloc(size_t floats);

@@ -35,7 +35,11 @@ class spk_model_config_t(ctypes.Structure):
                 ('m_channels', ctypes.c_int32), ('base_width', ctypes.c_int32), ('scale', ctypes.c_int32),
                 ('expansion', ctypes.c_int32), ('two_emb_layer', ctypes.c_int32),
                 ('channels', ctypes.c_int32 * 5), ('kernel_sizes', ctypes.c_int32 * 5),
-                ('dilations', ctypes.c_int32 * 5), ('reserved', ctypes.c_int32 * 8)]
+                ('dilations', ctypes.c_int32 * 5), ('precision', ctypes.c_int32), ('reserved', ctypes.c_int32 * 7)]
+
+
+# spk_model_config_t.precision (include/spk_hip.h)
+PRECISIONS = {'fp32': 0, 'fp16': 1}
 
 
 SPK_CONSUME_TOPK = 1
@@ -204,9 +208,13 @@ def fbank_padded(wavs: torch.Tensor, lengths, n_mels: int = 80, mean_nor: bool =
 class NativeModel:
     """One ``spk_model_t`` handle (folded + packed weights on one device)."""
 
-    def __init__(self, arch: int, cfg: dict, state_dict, device: torch.device):
+    def __init__(self, arch: int, cfg: dict, state_dict, device: torch.device, precision: str = 'fp32'):
+        if precision not in PRECISIONS:
+            raise HipError(f'precision must be one of {sorted(PRECISIONS)}, got {precision!r}')
         c = spk_model_config_t()
         c.arch = arch
+        c.precision = PRECISIONS[precision]
+        self.precision = precision
         for k in ('feat_dim', 'embed_dim', 'm_channels', 'base_width', 'scale', 'expansion', 'two_emb_layer'):
             setattr(c, k, int(cfg.get(k, 0)))
         for k in ('channels', 'kernel_sizes', 'dilations'):
@@ -359,12 +367,24 @@ class HipModuleMixin:
     def _hip_reset(self, *args, **kwargs):
         self.__dict__['_hip_handles'] = {}
 
+    def set_hip_precision(self, precision: str):
+        """'fp32' (default): fp32-accurate forward (fp16x3 split products), embeddings within
+        1e-4 of the reference.  'fp16': one fp16 MFMA product per multiply with fp32
+        accumulation -- the reduced-precision mode of BASELINE config C3 (cosine >= 0.9999 to
+        the reference); layers without a single-product kernel stay fp16x3."""
+        if precision not in PRECISIONS:
+            raise HipError(f'precision must be one of {sorted(PRECISIONS)}, got {precision!r}')
+        self.__dict__['_hip_precision'] = precision
+        self._hip_reset()
+        return self
+
     def _hip_handle(self, device: torch.device) -> NativeModel:
         handles = self.__dict__.setdefault('_hip_handles', {})
         key = (device.type, device.index)
         h = handles.get(key)
         if h is None:
-            h = NativeModel(self._hip_arch, self._hip_config(), self.state_dict(), device)
+            h = NativeModel(self._hip_arch, self._hip_config(), self.state_dict(), device,
+                            self.__dict__.get('_hip_precision', 'fp32'))
             handles[key] = h
         return h
 

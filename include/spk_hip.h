@@ -65,6 +65,9 @@ typedef struct {
 } spk_weight_t;
 
 /* Constructor arguments of the reference module (only those that shape the graph). */
+#define SPK_PRECISION_FP32 0
+#define SPK_PRECISION_FP16 1
+
 typedef struct {
   int32_t arch;
   int32_t feat_dim;       /* 80 */
@@ -77,7 +80,11 @@ typedef struct {
   int32_t channels[5];    /* ECAPA: channels */
   int32_t kernel_sizes[5];/* ECAPA: kernel_sizes */
   int32_t dilations[5];   /* ECAPA: dilations */
-  int32_t reserved[8];
+  int32_t precision;      /* SPK_PRECISION_FP32 (0, default): fp32-accurate (fp16x3 split
+                             products); SPK_PRECISION_FP16 (1): one fp16 MFMA product per
+                             multiply, fp32 accumulation -- BASELINE config C3's reduced-
+                             precision mode (cosine >= 0.9999 to the reference) */
+  int32_t reserved[7];
 } spk_model_config_t;
 
 int spk_version(void);

@@ -7,7 +7,7 @@
   c1   ECAPA-TDNN batch=32 2 s (the reference's CPU config, here on the GPU).
   models  every architecture at B=256, 2 s.
 
-    python tools/bench_workloads.py c3 [--steps K] [--warmup W] [--buckets 8]
+    python tools/bench_workloads.py c3 [--steps K] [--warmup W] [--buckets 4] [--precision fp32|fp16]
 """
 import argparse
 import json
@@ -55,7 +55,7 @@ def c3(args, device):
     for i, j in enumerate(order):
         host[i, :lens_sorted[i]] = synthetic.synth_wav(int(lens_sorted[i]), seed=2_000_000 + int(j))
     wavs = torch.from_numpy(host).to(device)
-    model = load('campplus', device)
+    model = load('campplus', device).set_hip_precision(args.precision)
     bounds = np.linspace(0, n, args.buckets + 1).astype(int)
     buckets = []
     for a, b in zip(bounds[:-1], bounds[1:]):
@@ -78,7 +78,8 @@ def c3(args, device):
             'lengths': '1-5 s ~U{16000..80000} samples, seed 2', 'ms_per_step': round(dt * 1e3, 3),
             'value': round(n / dt, 1), 'unit': 'utt/s (variable length)',
             'two_s_equivalent_per_s': round(audio_s / 2 / dt, 1), 'approx_tflops': round(flops / dt / 1e12, 2),
-            'dtype': 'f32 (fp16x3 MFMA)', 'data': 'synthetic'}
+            'dtype': 'f32 (fp16x3 MFMA)' if args.precision == 'fp32' else
+            'fp16 single-product MFMA, fp32 accumulate (C3 reduced-precision mode)', 'data': 'synthetic'}
 
 
 def c1(args, device):
@@ -109,7 +110,9 @@ def main():
     ap.add_argument('workload', choices=['c3', 'c1', 'models'])
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--buckets', type=int, default=8)
+    ap.add_argument('--buckets', type=int, default=4)
+    ap.add_argument('--precision', choices=['fp32', 'fp16'], default='fp32',
+                    help="c3: 'fp16' = the single-product mode (set_hip_precision)")
     args = ap.parse_args()
     device = torch.device('cuda', 0)
     torch.cuda.set_device(device)
