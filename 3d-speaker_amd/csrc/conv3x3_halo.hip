@@ -302,22 +302,35 @@ conv3x3_halo_persistent_kernel(const ConvDesc d) {
 // channel halves go to the blocks b and b + 8 (same XCD, so the second halo read of a
 // tile is an L2 hit).  The halo loads are unconditional (clamped address, zero applied
 // from a mask at staging) so they stay in flight across the taps.
-template <int CIN, int PIX>
+//
+// KS = 2 k-groups: the LDS (halo + all nine taps of the weights, ~140 KB) allows one block
+// per CU, so with one wave per 32-pixel tile a SIMD would run a single wave and expose
+// every LDS and barrier latency.  Instead a second group of NW waves computes the same
+// output tiles over the other half of each tap's 16-deep k-steps; its partial sums meet
+// the first group's in LDS before the epilogue (two waves per SIMD, half the MFMA chain
+// per wave, halo staging spread over twice the threads).
+template <int CIN, int PIX, int KS>
 struct HaloX3Cfg {
-  static constexpr int NP = 32, NW = PIX / 32, NT = 64 * NW;
+  static constexpr int NP = 32, NW = PIX / 32, NT = 64 * NW * KS;
   static constexpr int CINP = (CIN + 15) / 16 * 16, ROW = CINP + 8, QP = CINP / 4, Q = CIN / 4;
+  static constexpr int KSTEPS = CINP / 16, KSG = KSTEPS / KS;       // k-steps per tap / per group
+  static_assert(KSTEPS % KS == 0, "k-steps must split evenly over the groups");
   static constexpr int HALO_PIX = PIX == 256 ? 340 : 204;          // (TH+2)(TW+2), TW in {8, 16, 32}
   static constexpr int HALO_F = HALO_PIX * ROW;                     // floats = hi + lo halves
   static constexpr int WRES_F = 9 * NP * ROW;                       // floats = hi + lo halves
-  static constexpr int EPI = NW * 1024;
+  static constexpr int EPI = NW * 1024 * KS;                        // epilogue slabs + partner sums
   static constexpr int LDS = (HALO_F > EPI ? HALO_F : EPI) + WRES_F;
   static constexpr int PF = (HALO_PIX * QP + NT - 1) / NT;          // staged float4 per thread
 };
 
-template <int CIN, int TW, bool ADD, int PIX>
-__global__ void __launch_bounds__(64 * (PIX / 32), 1)
+// two k-groups where a tap has four k-steps (52 / 64 channels: -8 % per launch on
+// ERes2NetV2 layer2); with two k-steps (28 / 32) measured neutral to +1 %, so one group
+constexpr int halo_ks(int cin) { return cin > 32 ? 2 : 1; }
+
+template <int CIN, int TW, bool ADD, int PIX, int KS>
+__global__ void __launch_bounds__(64 * (PIX / 32) * KS, 1)
 conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
-  using C = HaloX3Cfg<CIN, PIX>;
+  using C = HaloX3Cfg<CIN, PIX, KS>;
   typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
   typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) float lds[C::LDS];
@@ -418,9 +431,10 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
     const int n = n0 + (lane & 7) * 4;
     if (d.bias && n < d.N) bias4 = *reinterpret_cast<const f32x4*>(d.bias + n);
   }
-  const int p_own = wave * 32 + li;
-  const int abase = ((p_own / TW) * HW + (p_own % TW)) * C::ROW + 8 * lh;
-  const int bbase = li * C::ROW + 8 * lh;
+  const int kg = wave / C::NW, pw = wave % C::NW;                  // k-group, pixel wave
+  const int p_own = pw * 32 + li;
+  const int abase = ((p_own / TW) * HW + (p_own % TW)) * C::ROW + 8 * lh + 16 * C::KSG * kg;
+  const int bbase = li * C::ROW + 8 * lh + 16 * C::KSG * kg;
   for (; t < ntiles; t += tstride) {
     const int tn = t + tstride;
 #if SPK_EXP != 1
@@ -434,7 +448,7 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
       const int aoff = abase + ((tap / 3) * HW + (tap % 3)) * C::ROW;
       const int boff = tap * C::NP * C::ROW + bbase;
 #pragma unroll
-      for (int s = 0; s < C::CINP / 16; ++s) {
+      for (int s = 0; s < C::KSG; ++s) {
         const f16x8 ah = *reinterpret_cast<const f16x8*>(hh + aoff + 16 * s);
         const f16x8 al = *reinterpret_cast<const f16x8*>(hlo + aoff + 16 * s);
         const f16x8 bh = *reinterpret_cast<const f16x8*>(wh + boff + 16 * s);
@@ -446,12 +460,24 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
     }
     acc[0][0] += accx * (1.0f / 2048.0f);
     __syncthreads();                                // halo reads done: the epilogue reuses it
-    {
+    if constexpr (KS > 1) {                         // group 1's partial sums -> group 0
+      float* part = lds + (C::NW + pw) * 1024;
+      if (kg == 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) part[r * 64 + lane] = acc[0][0][r];
+      }
+      __syncthreads();
+      if (kg == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[0][0][r] += part[r * 64 + lane];
+      }
+    }
+    if (kg == 0) {
       const int img = t / (ntx * nty), ty = (t / ntx) % nty, tx = t % ntx;
       const int y0 = ty * TH, x0 = tx * TW;
 #if SPK_EXP != 2
-      epilogue_tiles<1, 1, true>(d, lds, acc, wave, lane, n0, d.nimg * H * W, [&](int r) {
-        const int p = wave * 32 + r;
+      epilogue_tiles<1, 1, true>(d, lds, acc, pw, lane, n0, d.nimg * H * W, [&](int r) {
+        const int p = pw * 32 + r;
         const int gy = y0 + p / TW, gx = x0 + p % TW;
         return (gy < H && gx < W) ? (img * H + gy) * W + gx : -1;
       }, &bias4);
@@ -487,7 +513,7 @@ int resident_blocks(K kernel, int threads) {
 
 template <int CIN, int TW, int PIX>
 hipError_t launch_halo_x3_tw(const ConvDesc& d, hipStream_t s) {
-  constexpr int TH = PIX / TW, NT = 64 * (PIX / 32);
+  constexpr int TH = PIX / TW, NT = HaloX3Cfg<CIN, PIX, halo_ks(CIN)>::NT;
   const int tiles = d.nimg * ((d.Ho + TH - 1) / TH) * ((d.Wo + TW - 1) / TW);
   const int nsplit = (d.N + 31) / 32;
   auto grid_for = [&](int per_cu) {
@@ -497,11 +523,11 @@ hipError_t launch_halo_x3_tw(const ConvDesc& d, hipStream_t s) {
     return g * nsplit;
   };
   if (d.s0.p2) {
-    auto k = conv3x3_halo_x3_kernel<CIN, TW, true, PIX>;
+    auto k = conv3x3_halo_x3_kernel<CIN, TW, true, PIX, halo_ks(CIN)>;
     static const int per_cu = resident_blocks(k, NT);
     hipLaunchKernelGGL(k, dim3(grid_for(per_cu)), dim3(NT), 0, s, d, nsplit);
   } else {
-    auto k = conv3x3_halo_x3_kernel<CIN, TW, false, PIX>;
+    auto k = conv3x3_halo_x3_kernel<CIN, TW, false, PIX, halo_ks(CIN)>;
     static const int per_cu = resident_blocks(k, NT);
     hipLaunchKernelGGL(k, dim3(grid_for(per_cu)), dim3(NT), 0, s, d, nsplit);
   }
@@ -615,7 +641,7 @@ std::string halo_kernel_name(const ConvDesc& d) {
   if (x3_halo_ok(d)) {
     const int px = 128;
     return "conv3x3_halo_x3_kernel<" + std::to_string(d.s0.cin) + ", " + std::to_string(pick_tw(d.Ho, d.Wo, px)) +
-           ", " + (add ? "true" : "false") + ", " + std::to_string(px) + ">";
+           ", " + (add ? "true" : "false") + ", " + std::to_string(px) + ", " + std::to_string(halo_ks(d.s0.cin)) + ">";
   }
   if (persistent_ok(d))
     return "conv3x3_halo_persistent_kernel<" + std::to_string(d.s0.cin) + ", " + std::to_string(tw) + ", " +

@@ -134,33 +134,42 @@ struct ERes2Builder {
   }
 
   // The whole block as one fused kernel (res2block.hip): ERes2NetV2 stage-1 shape (scale 2,
-  // identity shortcut, 128 channels, slices <= 32 wide), fp16x3 path, uniform lengths.
+  // slices <= 32 wide, 128 output channels) -- identity shortcut from 128 channels, or the
+  // stage's first block with a 1x1 stride-1 projection shortcut from 64 -- fp16x3 path,
+  // uniform lengths.
   bool fusable(const std::string& p, const T4& x, int stride, int width, int Cout, bool use_aff) const {
-    return v2 && !use_aff && stride == 1 && scale == 2 && width <= 32 && x.C == 128 && Cout == 128 &&
-           x.ld == x.C && !m.has(p + ".shortcut.0.weight") && !b.ragged && b.x3() &&
-           std::getenv("SPK_NO_BLOCK_FUSION") == nullptr;
+    const bool sc = m.has(p + ".shortcut.0.weight");
+    const bool shape = sc ? (x.C == 64 && std::getenv("SPK_NO_PROJ_FUSION") == nullptr) : x.C == 128;
+    return v2 && !use_aff && stride == 1 && scale == 2 && width <= 32 && shape && Cout == 128 &&
+           x.ld == x.C && !b.ragged && b.x3() && std::getenv("SPK_NO_BLOCK_FUSION") == nullptr;
   }
 
-  T4 fused_block(const std::string& p, const T4& x, int width, Buf outbuf) {
+  T4 fused_block(const std::string& p, const T4& x, int width, int Cout, Buf outbuf) {
     const ChanMap xin = ChanMap::dense(x.C);
+    const ChanMap om = ChanMap::dense(Cout);
     const ChanMap sl = ChanMap::slices(width, 2, 32);
     const ChanMap w32 = ChanMap::dense(width, 32);
+    const bool proj = m.has(p + ".shortcut.0.weight");
     const Packed& c1 = m.pack(p + ".conv1#fused", sl, {Part{p + ".conv1.weight", "", p + ".bn1", xin, 0, 0}}, x.C);
     const Packed& ca = m.pack(p + ".convs.0#fused", w32, {Part{p + ".convs.0.weight", "", p + ".bns.0", w32, 0, 0}}, 9 * 32);
     const Packed& cb = m.pack(p + ".convs.1#fused", w32, {Part{p + ".convs.1.weight", "", p + ".bns.1", w32, 0, 0}}, 9 * 32);
-    const Packed& c3 = m.pack(p + ".conv3#fused", xin, {Part{p + ".conv3.weight", "", p + ".bn3", sl, 0, 0}}, 64);
+    std::vector<Part> parts3{Part{p + ".conv3.weight", "", p + ".bn3", sl, 0, 0}};
+    if (proj) parts3.push_back(Part{p + ".shortcut.0.weight", "", p + ".shortcut.1", xin, 0, 64});
+    const Packed& c3 = m.pack(p + ".conv3#fused", om, parts3, 64 + (proj ? x.C : 0));
     const double px = (double)x.H * x.W;
-    b.macs_per_utt += px * x.C * (double)width * 2 + 2.0 * px * 9.0 * width * width + px * (double)width * 2 * x.C;
-    T4 out{outbuf, x.C, x.H, x.W, x.C};
+    b.macs_per_utt += px * x.C * (double)width * 2 + 2.0 * px * 9.0 * width * width + px * (double)width * 2 * Cout +
+                      (proj ? px * x.C * (double)Cout : 0.0);
+    T4 out{outbuf, Cout, x.H, x.W, Cout};
     if (b.plan) {
       Res2Desc d;
       d.nimg = b.B; d.H = x.H; d.W = x.W; d.C = x.C; d.width = width;
+      d.Cout = Cout; d.proj = proj;
       d.w1h = m.dhi(c1.w_off); d.w1l = m.dlo(c1.w_off); d.b1 = m.dptr(c1.b_off);
       d.wah = m.dhi(ca.w_off); d.wal = m.dlo(ca.w_off); d.ba = m.dptr(ca.b_off);
       d.wbh = m.dhi(cb.w_off); d.wbl = m.dlo(cb.w_off); d.bb = m.dptr(cb.b_off);
       d.w3h = m.dhi(c3.w_off); d.w3l = m.dlo(c3.w_off); d.b3 = m.dptr(c3.b_off);
       d.w1 = m.dptr(c1.w_off); d.wa = m.dptr(ca.w_off); d.wb = m.dptr(cb.w_off); d.w3 = m.dptr(c3.w_off);
-      const double bytes = 8.0 * b.B * px * x.C +
+      const double bytes = 4.0 * b.B * px * (x.C + Cout) +
                            4.0 * ((double)c1.N * c1.K + (double)ca.N * ca.K + (double)cb.N * cb.K + (double)c3.N * c3.K);
       const Buf xb = x.buf, ob = outbuf;
       b.step(p + ".fused", [d, xb, ob](const Ctx& c) mutable {
@@ -175,7 +184,7 @@ struct ERes2Builder {
   T4 block(const std::string& p, const T4& x, int stride, int width, int planes, bool use_aff, Buf outbuf) {
     const int Ho = (x.H - 1) / stride + 1, Wo = (x.W - 1) / stride + 1;
     const int Cout = planes * expansion;
-    if (fusable(p, x, stride, width, Cout, use_aff)) return fused_block(p, x, width, outbuf);
+    if (fusable(p, x, stride, width, Cout, use_aff)) return fused_block(p, x, width, Cout, outbuf);
     const ChanMap sl = ChanMap::slices(width, scale);
     const int wp = sl.n_phys / scale;
     const int ldt = sl.n_phys;

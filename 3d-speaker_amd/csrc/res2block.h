@@ -12,15 +12,18 @@
 namespace spk {
 
 struct Res2Desc {
-  const float* x = nullptr;     // block input and residual, channels-last [nimg, H, W, C]
-  float* out = nullptr;         // [nimg, H, W, C]
+  const float* x = nullptr;     // block input (and residual), channels-last [nimg, H, W, C]
+  float* out = nullptr;         // [nimg, H, W, Cout]
   int nimg = 0, H = 0, W = 0, C = 0;
+  int Cout = 0;                 // output channels (0: C)
+  bool proj = false;            // 1x1 projection shortcut + BN (ERes2NetV2.py:84-88), packed
+                                // into w3 as K columns 64 .. 64+C, its BN shift into b3
   int width = 0;                // Res2Net slice width (26 for ERes2NetV2 layer1), <= 32
   // fp16 hi / lo planes of the BN-folded packed weights (Model::pack) and fp32 biases:
   const uint16_t* w1h = nullptr; const uint16_t* w1l = nullptr; const float* b1 = nullptr;   // [64][C]
   const uint16_t* wah = nullptr; const uint16_t* wal = nullptr; const float* ba = nullptr;   // convs.0 [32][9*32]
   const uint16_t* wbh = nullptr; const uint16_t* wbl = nullptr; const float* bb = nullptr;   // convs.1 [32][9*32]
-  const uint16_t* w3h = nullptr; const uint16_t* w3l = nullptr; const float* b3 = nullptr;   // [C][64]
+  const uint16_t* w3h = nullptr; const uint16_t* w3l = nullptr; const float* b3 = nullptr;   // [Cout][64 (+C)]
   const float* w1 = nullptr; const float* wa = nullptr;   // the same four matrices in fp32 (the
   const float* wb = nullptr; const float* w3 = nullptr;   // host emulation of the kernel reads them)
 };

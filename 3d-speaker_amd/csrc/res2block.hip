@@ -1,5 +1,8 @@
 // Fused ERes2NetV2 Res2Net block (speakerlab/models/eres2net/ERes2NetV2.py:65-91) for the
-// stage-1 blocks with an identity shortcut: one persistent kernel, fp16x3 MFMA, gfx950.
+// stage-1 blocks: one persistent kernel, fp16x3 MFMA, gfx950.  Two shapes: the identity-
+// shortcut blocks (128 -> 128 channels) and the first block of the stage (64 -> 128, a 1x1
+// projection shortcut + BN, ERes2NetV2.py:84-88), whose shortcut GEMM is K-concatenated
+// with conv3 (K = 64 concat channels + 64 input channels, biases summed on the host).
 //
 // Unfused, a stage-1 block is four launches (conv1, two 3x3 convs, conv3 + residual) whose
 // intermediates make full HBM round trips: ~2.5 KB per pixel for 0.5 KB of real input and
@@ -12,7 +15,9 @@
 //   2. convs.0 (3x3) + bn + Hardtanh on the 10 x 18 halo-1 region; sp = y0 + s1 is formed
 //      in place in SP (torch: sp = sp + spx[1]), y0's centre goes to CAT;
 //   3. convs.1 (3x3) + bn + Hardtanh on the 8 x 16 tile -> CAT;
-//   4. conv3 (1x1, 64 -> C) + bn3 + residual + Hardtanh -> HBM.
+//   4. conv3 (1x1, 64 -> CO) + bn3 + residual + Hardtanh -> HBM; with the projection
+//      shortcut the tile's input pixels are staged into LDS (over the SP region, free
+//      after convs.1) as conv3's second K half, and no residual is read.
 // Halo recompute: conv1 runs on 240 pixels and convs.0 on 180 per 128 outputs.
 //
 // MFMA v_mfma_f32_16x16x32_f16 in the TRANSPOSED form out^T[n][px] = W[n][k] . In^T[k][px]:
@@ -46,7 +51,7 @@ namespace {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-template <int C>
+template <int CI, int CO, bool PROJ>
 struct R2 {
   static constexpr int NT = 512;
   static constexpr int TH = 8, TW = 16;
@@ -55,16 +60,22 @@ struct R2 {
   static constexpr int NO = TH * TW;                                // 128 output px
   static constexpr int XCH = 32;                                    // pixels per conv1 input chunk
   static constexpr int NCH = (NR + XCH - 1) / XCH;                  // 8 chunks
-  static constexpr int XF = XCH * (C / 4) / NT;                     // float4 staged per thread per chunk
-  static constexpr int KS1 = C / 32;                                // conv1 k-steps
-  static constexpr int NT3 = C / 128;                               // conv3 n-tiles per wave
+  static constexpr int XF = XCH * (CI / 4) / NT;                    // float4 staged per thread per chunk
+  static constexpr int KS1 = CI / 32;                               // conv1 k-steps
+  static constexpr int NT3 = CO / 128;                              // conv3 n-tiles per wave
+  static constexpr int KS3 = PROJ ? 2 + CI / 32 : 2;                // conv3 k-steps (concat | input)
+  static constexpr int K3 = 32 * KS3;                               // packed conv3 row length
+  static constexpr int CSW = CI / 8 - 1 < 15 ? CI / 8 - 1 : 15;     // chunk-row swizzle mask
+  static constexpr int XCEN_PL = NO * CI;                           // PROJ: staged input tile (halves)
   static constexpr int S0_PL = NR * 32, CAT_PL = NO * 64;           // plane sizes (halves)
   static constexpr int R0_PL = S0_PL > CAT_PL ? S0_PL : CAT_PL;
-  static constexpr int SP_PL = NP * 32, XC_PL = XCH * C, WC_PL = 2 * 32 * 288;
+  static constexpr int SP_PL = NP * 32, XC_PL = XCH * CI, WC_PL = 2 * 32 * 288;
   static constexpr int OFF_SP = 2 * R0_PL, OFF_XC = OFF_SP + 2 * SP_PL, OFF_WC = OFF_XC + 4 * XC_PL;
   static constexpr int LDS_HALVES = OFF_WC + 2 * WC_PL;
-  static_assert(C % 128 == 0, "conv3 n-tiles are dealt 8 per wave round");
-  static_assert(XCH * (C / 4) % NT == 0, "input chunk must split evenly over the block");
+  static_assert(CO % 128 == 0, "conv3 n-tiles are dealt 8 per wave round");
+  static_assert(XCH * (CI / 4) % NT == 0, "input chunk must split evenly over the block");
+  static_assert(PROJ ? (CI == 64 && OFF_SP + 2 * XCEN_PL <= OFF_WC) : CI == CO, "block shape");
+  static_assert(!PROJ || NO * (CI / 4) == 4 * NT, "PROJ: the input tile is four float4 per thread");
   static_assert(NCH >= 4, "the chunk ring assumes at least four chunks");
 };
 
@@ -74,10 +85,10 @@ __device__ __forceinline__ f32x4 mfma16(const f16x8& a, const f16x8& b, const f3
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-template <int C>
+template <int CI, int CO, bool PROJ>
 __global__ void __launch_bounds__(512, 1)
 res2_block_kernel(const Res2Desc d) {
-  using G = R2<C>;
+  using G = R2<CI, CO, PROJ>;
   __shared__ __attribute__((aligned(16))) _Float16 lds[G::LDS_HALVES];
   _Float16* const S0h = lds;                  // S0 region, then (aliased) CAT
   _Float16* const S0l = lds + G::S0_PL;
@@ -89,6 +100,8 @@ res2_block_kernel(const Res2Desc d) {
   _Float16* const XCl = XCh + 2 * G::XC_PL;
   _Float16* const WCh = lds + G::OFF_WC;
   _Float16* const WCl = WCh + G::WC_PL;
+  _Float16* const XNh = lds + G::OFF_SP;      // PROJ: the tile's input pixels (over SP + XC)
+  _Float16* const XNl = XNh + G::XCEN_PL;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, lq = lane >> 4;
@@ -118,18 +131,18 @@ res2_block_kernel(const Res2Desc d) {
   f16x8 a1h[G::KS1], a1l[G::KS1];
 #pragma unroll
   for (int ks = 0; ks < G::KS1; ++ks) {
-    const size_t o = (size_t)(16 * nt1 + l16) * C + 32 * ks + 8 * lq;
+    const size_t o = (size_t)(16 * nt1 + l16) * CI + 32 * ks + 8 * lq;
     a1h[ks] = *reinterpret_cast<const f16x8*>(d.w1h + o);
     a1l[ks] = *reinterpret_cast<const f16x8*>(d.w1l + o);
   }
-  f16x8 a3h[G::NT3][2], a3l[G::NT3][2];
+  f16x8 a3h[G::NT3][G::KS3], a3l[G::NT3][G::KS3];
   f32x4 b3v[G::NT3];
 #pragma unroll
   for (int j = 0; j < G::NT3; ++j) {
     const int n = 16 * (wave + 8 * j);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const size_t o = (size_t)(n + l16) * 64 + 32 * ks + 8 * lq;
+    for (int ks = 0; ks < G::KS3; ++ks) {
+      const size_t o = (size_t)(n + l16) * G::K3 + 32 * ks + 8 * lq;
       a3h[j][ks] = *reinterpret_cast<const f16x8*>(d.w3h + o);
       a3l[j][ks] = *reinterpret_cast<const f16x8*>(d.w3l + o);
     }
@@ -151,18 +164,18 @@ res2_block_kernel(const Res2Desc d) {
 #pragma unroll
     for (int j = 0; j < G::XF; ++j) {
       const int i = tid + G::NT * j;
-      const int px = ch * G::XCH + i / (C / 4), q = i % (C / 4);
+      const int px = ch * G::XCH + i / (CI / 4), q = i % (CI / 4);
       const int gy = min(max(ty0 - 2 + px / G::RW, 0), H - 1);
       const int gx = min(max(tx0 - 2 + px % G::RW, 0), W - 1);
-      v[j] = *reinterpret_cast<const f32x4*>(im + ((size_t)gy * W + gx) * C + 4 * q);
+      v[j] = *reinterpret_cast<const f32x4*>(im + ((size_t)gy * W + gx) * CI + 4 * q);
     }
   };
   auto store_chunk = [&](const f32x4 (&v)[G::XF], int buf) {
 #pragma unroll
     for (int j = 0; j < G::XF; ++j) {
       const int i = tid + G::NT * j;
-      const int px = i / (C / 4), q = i % (C / 4);
-      const int a = buf * G::XC_PL + px * C + 8 * ((q >> 1) ^ (px & 15)) + 4 * (q & 1);
+      const int px = i / (CI / 4), q = i % (CI / 4);
+      const int a = buf * G::XC_PL + px * CI + 8 * ((q >> 1) ^ (px & G::CSW)) + 4 * (q & 1);
       h16x4 h, l;
       split_x3(v[j], h, l);
       *reinterpret_cast<h16x4*>(XCh + a) = h;
@@ -178,7 +191,7 @@ res2_block_kernel(const Res2Desc d) {
   if (t_lo + slot < t_hi) {
     int im, ty0, tx0;
     tile_origin(t_lo + slot, im, ty0, tx0);
-    const float* p0 = d.x + (size_t)im * H * W * C;
+    const float* p0 = d.x + (size_t)im * H * W * CI;
     load_chunk(0, pf[0], ty0, tx0, p0);
     load_chunk(1, pf[1], ty0, tx0, p0);
     load_chunk(2, pf[2], ty0, tx0, p0);
@@ -186,7 +199,7 @@ res2_block_kernel(const Res2Desc d) {
   for (int t = t_lo + slot; t < t_hi; t += nslot) {
     int img, y0, x0;
     tile_origin(t, img, y0, x0);
-    const float* const xim = d.x + (size_t)img * H * W * C;
+    const float* const xim = d.x + (size_t)img * H * W * CI;
 
     // ================= 1. conv1 on the S0 region, 32 pixels per chunk: chunks are staged
     //   through two LDS buffers (fp16 hi / lo, rows swizzled block ^ (px & 15)), their global
@@ -211,7 +224,7 @@ res2_block_kernel(const Res2Desc d) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accx = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < G::KS1; ++ks) {
-        const int a = pxl * C + 8 * ((4 * ks + lq) ^ (pxl & 15));
+        const int a = pxl * CI + 8 * ((4 * ks + lq) ^ (pxl & G::CSW));
         const f16x8 bh = *reinterpret_cast<const f16x8*>(xh + a);
         const f16x8 bl = *reinterpret_cast<const f16x8*>(xl + a);
         acc = mfma16(a1h[ks], bh, acc);
@@ -315,12 +328,19 @@ res2_block_kernel(const Res2Desc d) {
     __syncthreads();
     R2_STAMP(4);
 
-    // residual of the first half of the conv3 pixel tiles: requested now, in flight during convs.1
+    // residual of the first half of the conv3 pixel tiles (PROJ: the tile's input pixels,
+    // conv3's second operand): requested now, in flight during convs.1
     f32x4 res_a[4];
 #pragma unroll
     for (int pt = 0; pt < 4; ++pt) {
-      const int gy = min(y0 + pt, H - 1), gx = min(x0 + l16, W - 1);
-      res_a[pt] = *reinterpret_cast<const f32x4*>(xim + ((size_t)gy * W + gx) * C + 16 * wave + 4 * lq);
+      if constexpr (PROJ) {
+        const int i = tid + G::NT * pt, o = i / (CI / 4), q = i % (CI / 4);
+        const int gy = min(y0 + o / G::TW, H - 1), gx = min(x0 + o % G::TW, W - 1);
+        res_a[pt] = *reinterpret_cast<const f32x4*>(xim + ((size_t)gy * W + gx) * CI + 4 * q);
+      } else {
+        const int gy = min(y0 + pt, H - 1), gx = min(x0 + l16, W - 1);
+        res_a[pt] = *reinterpret_cast<const f32x4*>(xim + ((size_t)gy * W + gx) * CI + 16 * wave + 4 * lq);
+      }
     }
 
     // ================= 3. convs.1 on the output tile (2 pixel tiles per wave)
@@ -368,6 +388,18 @@ res2_block_kernel(const Res2Desc d) {
       }
     }
     __syncthreads();
+    if constexpr (PROJ) {                     // SP / XC reads done: stage the input tile there
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt) {
+        const int i = tid + G::NT * pt, o = i / (CI / 4), q = i % (CI / 4);
+        const int a = o * CI + 8 * ((q >> 1) ^ (o & 7)) + 4 * (q & 1);
+        h16x4 h, l;
+        split_x3(res_a[pt], h, l);
+        *reinterpret_cast<h16x4*>(XNh + a) = h;
+        *reinterpret_cast<h16x4*>(XNl + a) = l;
+      }
+      __syncthreads();
+    }
     R2_STAMP(5);
 
     // ================= 4. conv3 + bn3 + residual + Hardtanh -> out (8 pixel tiles per wave)
@@ -376,14 +408,15 @@ res2_block_kernel(const Res2Desc d) {
 #pragma unroll
     for (int pt = 0; pt < 4; ++pt) {
       const int gy = min(y0 + 4 + pt, H - 1), gx = min(x0 + l16, W - 1);
-      res_b[pt] = *reinterpret_cast<const f32x4*>(xim + ((size_t)gy * W + gx) * C + 16 * wave + 4 * lq);
+      if constexpr (PROJ) res_b[pt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      else res_b[pt] = *reinterpret_cast<const f32x4*>(xim + ((size_t)gy * W + gx) * CI + 16 * wave + 4 * lq);
     }
     // the next tile's first three input chunks, behind the residual (vmcnt retires in order,
     // so the epilogue's wait for the residual does not wait for these)
     if (t + nslot < t_hi) {
       int im, ty0, tx0;
       tile_origin(t + nslot, im, ty0, tx0);
-      const float* pn = d.x + (size_t)im * H * W * C;
+      const float* pn = d.x + (size_t)im * H * W * CI;
       load_chunk(0, pf[0], ty0, tx0, pn);
       load_chunk(1, pf[1], ty0, tx0, pn);
       load_chunk(2, pf[2], ty0, tx0, pn);
@@ -396,10 +429,17 @@ res2_block_kernel(const Res2Desc d) {
         const int o = 16 * pt + l16;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accx = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const int a = o * 64 + 8 * ((4 * ks + lq) ^ (o & 7));
-          const f16x8 bh = *reinterpret_cast<const f16x8*>(CATh + a);
-          const f16x8 bl = *reinterpret_cast<const f16x8*>(CATl + a);
+        for (int ks = 0; ks < G::KS3; ++ks) {
+          f16x8 bh, bl;
+          if (ks < 2) {
+            const int a = o * 64 + 8 * ((4 * ks + lq) ^ (o & 7));
+            bh = *reinterpret_cast<const f16x8*>(CATh + a);
+            bl = *reinterpret_cast<const f16x8*>(CATl + a);
+          } else {
+            const int a = o * CI + 8 * ((4 * (ks - 2) + lq) ^ (o & 7));
+            bh = *reinterpret_cast<const f16x8*>(XNh + a);
+            bl = *reinterpret_cast<const f16x8*>(XNl + a);
+          }
           acc = mfma16(a3h[j][ks], bh, acc);
           accx = mfma16(a3h[j][ks], bl, accx);
           accx = mfma16(a3l[j][ks], bh, accx);
@@ -408,8 +448,11 @@ res2_block_kernel(const Res2Desc d) {
         if (gy < H && gx < W) {
           f32x4 v;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = htanh(acc[e] + accx[e] * kLo + b3v[j][e] + (pt < 4 ? res_a[pt][e] : res_b[pt - 4][e]));
-          *reinterpret_cast<f32x4*>(d.out + (((size_t)img * H + gy) * W + gx) * C + n) = v;
+          for (int e = 0; e < 4; ++e) {
+            const float r = PROJ ? 0.f : (pt < 4 ? res_a[pt][e] : res_b[pt - 4][e]);
+            v[e] = htanh(acc[e] + accx[e] * kLo + b3v[j][e] + r);
+          }
+          *reinterpret_cast<f32x4*>(d.out + (((size_t)img * H + gy) * W + gx) * CO + n) = v;
         }
       }
     }
@@ -433,18 +476,23 @@ int device_cus_r2() {
 }  // namespace
 
 bool res2_block_supported(const Res2Desc& d) {
-  return conv_use_x3() && d.C == 128 && d.width >= 1 && d.width <= 32 && d.nimg > 0 && d.H > 0 && d.W > 0 &&
+  const int co = d.Cout ? d.Cout : d.C;
+  const bool shape = d.proj ? (d.C == 64 && co == 128) : (d.C == 128 && co == 128);
+  return conv_use_x3() && shape && d.width >= 1 && d.width <= 32 && d.nimg > 0 && d.H > 0 && d.W > 0 &&
          d.w1h && d.w1l && d.wah && d.wal && d.wbh && d.wbl && d.w3h && d.w3l && d.b1 && d.ba && d.bb && d.b3;
 }
 
-std::string res2_block_kernel_name(const Res2Desc& d) { return "res2_block_kernel<" + std::to_string(d.C) + ">"; }
+std::string res2_block_kernel_name(const Res2Desc& d) {
+  return d.proj ? "res2_block_kernel<64, 128, true>" : "res2_block_kernel<128, 128, false>";
+}
 
 hipError_t launch_res2_block(const Res2Desc& d, hipStream_t s) {
   if (!res2_block_supported(d) || d.x == d.out) return hipErrorInvalidValue;
   const int ntiles = d.nimg * ((d.W + 15) / 16) * ((d.H + 7) / 8);
   int grid = std::min(device_cus_r2(), (ntiles + 7) / 8 * 8);
   grid = std::max(8, grid / 8 * 8);
-  hipLaunchKernelGGL(res2_block_kernel<128>, dim3(grid), dim3(512), 0, s, d);
+  if (d.proj) hipLaunchKernelGGL((res2_block_kernel<64, 128, true>), dim3(grid), dim3(512), 0, s, d);
+  else hipLaunchKernelGGL((res2_block_kernel<128, 128, false>), dim3(grid), dim3(512), 0, s, d);
   return hipGetLastError();
 }
 

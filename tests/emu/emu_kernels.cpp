@@ -192,14 +192,17 @@ bool conv_use_x3() {
 
 // fused Res2Net block (res2block.hip), the kernel's contract in double precision:
 // conv1 + bn1 + Hardtanh -> s0 | s1 (32-channel slices), y0 = Ht(conv3x3(s0)),
-// y1 = Ht(conv3x3(y0 + s1)), out = Ht(conv3(cat(y0, y1)) + x), zero padding at the edges
+// y1 = Ht(conv3x3(y0 + s1)), out = Ht(conv3(cat(y0, y1)) + x) -- or, with the projection
+// shortcut, Ht(conv3(cat(y0, y1, x))) -- zero padding at the edges
 bool res2_block_supported(const Res2Desc& d) {
-  return d.C == 128 && d.width >= 1 && d.width <= 32 && d.w1 && d.wa && d.wb && d.w3 && d.b1 && d.ba && d.bb && d.b3;
+  const int co = d.Cout ? d.Cout : d.C;
+  const bool shape = d.proj ? (d.C == 64 && co == 128) : (d.C == 128 && co == 128);
+  return shape && d.width >= 1 && d.width <= 32 && d.w1 && d.wa && d.wb && d.w3 && d.b1 && d.ba && d.bb && d.b3;
 }
 std::string res2_block_kernel_name(const Res2Desc& d) { return "emu_res2_block<" + std::to_string(d.C) + ">"; }
 hipError_t launch_res2_block(const Res2Desc& d, hipStream_t) {
   if (!res2_block_supported(d) || d.x == d.out) return hipErrorInvalidValue;
-  const int H = d.H, W = d.W, C = d.C;
+  const int H = d.H, W = d.W, C = d.C, CO = d.Cout ? d.Cout : d.C, K3 = d.proj ? 64 + C : 64;
   auto ht = [](double v) { return std::min(std::max(v, 0.0), 20.0); };
   std::vector<double> t1((size_t)H * W * 64), y0((size_t)H * W * 32), sp((size_t)H * W * 32), y1((size_t)H * W * 32);
   auto conv3 = [&](const std::vector<double>& in, const float* w, const float* b, std::vector<double>& out) {
@@ -218,7 +221,7 @@ hipError_t launch_res2_block(const Res2Desc& d, hipStream_t) {
   };
   for (int img = 0; img < d.nimg; ++img) {
     const float* xi = d.x + (size_t)img * H * W * C;
-    float* oi = d.out + (size_t)img * H * W * C;
+    float* oi = d.out + (size_t)img * H * W * CO;
     for (size_t p = 0; p < (size_t)H * W; ++p)
       for (int n = 0; n < 64; ++n) {
         double acc = d.b1[n];
@@ -233,11 +236,13 @@ hipError_t launch_res2_block(const Res2Desc& d, hipStream_t) {
       for (int c = 0; c < 32; ++c) sp[p * 32 + c] = y0[p * 32 + c] + t1[p * 64 + 32 + c];
     conv3(sp, d.wb, d.bb, y1);
     for (size_t p = 0; p < (size_t)H * W; ++p)
-      for (int n = 0; n < C; ++n) {
-        double acc = d.b3[n] + xi[p * C + n];
+      for (int n = 0; n < CO; ++n) {
+        double acc = d.b3[n] + (d.proj ? 0.0 : xi[p * C + n]);
         for (int c = 0; c < 32; ++c)
-          acc += (double)d.w3[(size_t)n * 64 + c] * y0[p * 32 + c] + (double)d.w3[(size_t)n * 64 + 32 + c] * y1[p * 32 + c];
-        oi[p * C + n] = (float)ht(acc);
+          acc += (double)d.w3[(size_t)n * K3 + c] * y0[p * 32 + c] + (double)d.w3[(size_t)n * K3 + 32 + c] * y1[p * 32 + c];
+        if (d.proj)
+          for (int c = 0; c < C; ++c) acc += (double)d.w3[(size_t)n * K3 + 64 + c] * xi[p * C + c];
+        oi[p * CO + n] = (float)ht(acc);
       }
   }
   return hipSuccess;

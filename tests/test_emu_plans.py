@@ -77,8 +77,8 @@ def test_emulated_ragged_campplus_matches_per_utterance(arch):
 def test_step_bytes_priced_per_conv():
     """Per-step algorithmic bytes (the byte side of bench.py's per-launch roofline): every
     conv step is priced; ERes2NetV2 layer2.1.conv3 (1x1, 104 -> 256 channels, residual) is
-    exactly input + weights + output + residual, fp32, and the fused stage-1 block
-    layer1.1.fused is its input + output + the four packed weight matrices."""
+    exactly input + weights + output + residual, fp32, and the fused stage-1 blocks
+    layer1.1.fused / layer1.0.fused are their input + output + the packed weight matrices."""
     m = helpers.loaded_module('eres2netv2')
     em = EmuModel(m)
     B, T = 2, 40
@@ -94,3 +94,7 @@ def test_step_bytes_priced_per_conv():
     px = B * 80 * T
     w = 64 * 128 + 2 * 32 * 288 + 128 * 64
     assert nbytes[names.index('layer1.1.fused')] == 8.0 * px * 128 + 4.0 * w
+    # layer1.0 (64 -> 128, projection shortcut K-concatenated with conv3) is fused as well
+    w0 = 64 * 64 + 2 * 32 * 288 + 128 * 128
+    assert nbytes[names.index('layer1.0.fused')] == 4.0 * px * (64 + 128) + 4.0 * w0
+    assert not any(n.startswith('layer1.') and not n.endswith('.fused') for n in names)
