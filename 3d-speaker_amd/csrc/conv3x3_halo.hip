@@ -327,7 +327,7 @@ struct HaloX3Cfg {
 // ERes2NetV2 layer2); with two k-steps (28 / 32) measured neutral to +1 %, so one group
 constexpr int halo_ks(int cin) { return cin > 32 ? 2 : 1; }
 
-template <int CIN, int TW, bool ADD, int PIX, int KS>
+template <int CIN, int TW, bool ADD, int PIX, int KS, bool PLAIN>
 __global__ void __launch_bounds__(64 * (PIX / 32) * KS, 1)
 conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
   using C = HaloX3Cfg<CIN, PIX, KS>;
@@ -379,10 +379,19 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
 #pragma unroll
     for (int r = 0; r < C::PF; ++r) {
       const int gy = y0 + (int)(hrc[r] >> 16), gx = x0 + (int)(hrc[r] & 0xFFFFu);
-      const bool ok = (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+      const bool ok = ((unsigned)gy < (unsigned)H) & ((unsigned)gx < (unsigned)W);
       const uint32_t pix = (uint32_t)(gy * W + gx);
-      pa[r] = buf_load4(r0, ok ? (pix * (uint32_t)d.s0.ld + 4u * qq) * 4u : BUF_OOB);
-      if (ADD) pb[r] = buf_load4(r2, ok ? (pix * (uint32_t)d.s0.ld2 + 4u * qq) * 4u : BUF_OOB);
+      // offsets materialised in registers before the loads (the empty asm keeps the
+      // compiler from turning the select into a branch around the load: a load on only
+      // some paths leaves its wait count unknown, and every later wait becomes vmcnt(0))
+      uint32_t oa = ok ? (pix * (uint32_t)d.s0.ld + 4u * qq) * 4u : BUF_OOB;
+      asm volatile("" : "+v"(oa));
+      pa[r] = buf_load4(r0, oa);
+      if (ADD) {
+        uint32_t ob = ok ? (pix * (uint32_t)d.s0.ld2 + 4u * qq) * 4u : BUF_OOB;
+        asm volatile("" : "+v"(ob));
+        pb[r] = buf_load4(r2, ob);
+      }
     }
   };
   auto pf_store = [&]() {
@@ -406,6 +415,15 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
     }
   };
 
+  // the epilogue's bias quad, loaded once, before the first halo prefetch so that
+  // the first wait for the halo retires it too (otherwise the compiler keeps it pending and
+  // waits vmcnt(0) at its use in every tile; see epilogue_tiles: with the next tile's halo in
+  // flight, a per-tile bias load would wait for the whole prefetch)
+  f32x4 bias4 = {0.f, 0.f, 0.f, 0.f};
+  {
+    const int n = n0 + (lane & 7) * 4;
+    if (d.bias && n < d.N) bias4 = *reinterpret_cast<const f32x4*>(d.bias + n);
+  }
   int t = tbase;
   if (t < ntiles) pf_load(t);
   // all nine taps of this slice's split weights -> LDS ([tap][n][ROW] hi / lo); zero padded
@@ -424,13 +442,6 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
   if (t < ntiles) pf_store();
   __syncthreads();
 
-  // the epilogue's bias quad, loaded once (see epilogue_tiles: with the next tile's halo in
-  // flight, a per-tile bias load would wait for the whole prefetch)
-  f32x4 bias4 = {0.f, 0.f, 0.f, 0.f};
-  {
-    const int n = n0 + (lane & 7) * 4;
-    if (d.bias && n < d.N) bias4 = *reinterpret_cast<const f32x4*>(d.bias + n);
-  }
   const int kg = wave / C::NW, pw = wave % C::NW;                  // k-group, pixel wave
   const int p_own = pw * 32 + li;
   const int abase = ((p_own / TW) * HW + (p_own % TW)) * C::ROW + 8 * lh + 16 * C::KSG * kg;
@@ -476,7 +487,7 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
       const int img = t / (ntx * nty), ty = (t / ntx) % nty, tx = t % ntx;
       const int y0 = ty * TH, x0 = tx * TW;
 #if SPK_EXP != 2
-      epilogue_tiles<1, 1, true>(d, lds, acc, pw, lane, n0, d.nimg * H * W, [&](int r) {
+      epilogue_tiles<1, 1, true, PLAIN>(d, lds, acc, pw, lane, n0, d.nimg * H * W, [&](int r) {
         const int p = pw * 32 + r;
         const int gy = y0 + p / TW, gx = x0 + p % TW;
         return (gy < H && gx < W) ? (img * H + gy) * W + gx : -1;
@@ -511,27 +522,32 @@ int resident_blocks(K kernel, int threads) {
   return n;
 }
 
+template <int CIN, int TW, int PIX, bool ADD, bool PLAIN>
+hipError_t launch_halo_x3_k(const ConvDesc& d, int nsplit, int tiles, hipStream_t s) {
+  constexpr int NT = HaloX3Cfg<CIN, PIX, halo_ks(CIN)>::NT;
+  auto k = conv3x3_halo_x3_kernel<CIN, TW, ADD, PIX, halo_ks(CIN), PLAIN>;
+  static const int per_cu = resident_blocks(k, NT);
+  // nsplit blocks per tile group of 8; a multiple of 8 * nsplit (or everything when small)
+  const int slots = per_cu * device_cus();
+  const int g = std::min((tiles + 7) / 8 * 8, std::max(8, slots / nsplit / 8 * 8));
+  hipLaunchKernelGGL(k, dim3(g * nsplit), dim3(NT), 0, s, d, nsplit);
+  return hipGetLastError();
+}
+
+// PLAIN: no residual / post-affine / ragged mask, so the epilogue issues no load behind
+// the next tile's halo prefetch (conv_epilogue.h); the common case (every Res2Net 3x3)
 template <int CIN, int TW, int PIX>
 hipError_t launch_halo_x3_tw(const ConvDesc& d, hipStream_t s) {
-  constexpr int TH = PIX / TW, NT = HaloX3Cfg<CIN, PIX, halo_ks(CIN)>::NT;
+  constexpr int TH = PIX / TW;
   const int tiles = d.nimg * ((d.Ho + TH - 1) / TH) * ((d.Wo + TW - 1) / TW);
   const int nsplit = (d.N + 31) / 32;
-  auto grid_for = [&](int per_cu) {
-    // nsplit blocks per tile group of 8; a multiple of 8 * nsplit (or everything when small)
-    const int slots = per_cu * device_cus();
-    const int g = std::min((tiles + 7) / 8 * 8, std::max(8, slots / nsplit / 8 * 8));
-    return g * nsplit;
-  };
-  if (d.s0.p2) {
-    auto k = conv3x3_halo_x3_kernel<CIN, TW, true, PIX, halo_ks(CIN)>;
-    static const int per_cu = resident_blocks(k, NT);
-    hipLaunchKernelGGL(k, dim3(grid_for(per_cu)), dim3(NT), 0, s, d, nsplit);
-  } else {
-    auto k = conv3x3_halo_x3_kernel<CIN, TW, false, PIX, halo_ks(CIN)>;
-    static const int per_cu = resident_blocks(k, NT);
-    hipLaunchKernelGGL(k, dim3(grid_for(per_cu)), dim3(NT), 0, s, d, nsplit);
-  }
-  return hipGetLastError();
+  const bool plain = !d.res && !d.post_scale && !d.rowlen && !d.osplit &&
+                     ((double)d.nimg * d.Ho * d.Wo * d.ldo + d.N) * 4.0 < 0x7FFFFFF0;
+  if (d.s0.p2)
+    return plain ? launch_halo_x3_k<CIN, TW, PIX, true, true>(d, nsplit, tiles, s)
+                 : launch_halo_x3_k<CIN, TW, PIX, true, false>(d, nsplit, tiles, s);
+  return plain ? launch_halo_x3_k<CIN, TW, PIX, false, true>(d, nsplit, tiles, s)
+               : launch_halo_x3_k<CIN, TW, PIX, false, false>(d, nsplit, tiles, s);
 }
 
 template <int CIN, int PIX>
@@ -641,7 +657,9 @@ std::string halo_kernel_name(const ConvDesc& d) {
   if (x3_halo_ok(d)) {
     const int px = 128;
     return "conv3x3_halo_x3_kernel<" + std::to_string(d.s0.cin) + ", " + std::to_string(pick_tw(d.Ho, d.Wo, px)) +
-           ", " + (add ? "true" : "false") + ", " + std::to_string(px) + ", " + std::to_string(halo_ks(d.s0.cin)) + ">";
+           ", " + (add ? "true" : "false") + ", " + std::to_string(px) + ", " + std::to_string(halo_ks(d.s0.cin)) + ", " +
+           ((!d.res && d.ldr == 0 && !d.post_scale && !d.rowlen && !d.osplit &&
+             ((double)d.nimg * d.Ho * d.Wo * d.ldo + d.N) * 4.0 < 0x7FFFFFF0) ? "true" : "false") + ">";
   }
   if (persistent_ok(d))
     return "conv3x3_halo_persistent_kernel<" + std::to_string(d.s0.cin) + ", " + std::to_string(tw) + ", " +

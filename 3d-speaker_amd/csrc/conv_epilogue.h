@@ -70,7 +70,11 @@ __device__ __forceinline__ float epilogue_elem(const ConvDesc& d, int m, int n, 
 // `pre_bias` (optional, fast path): the lane's bias quads per tile, loaded by the caller
 // ahead of time.  A persistent kernel with the next tile's loads in flight must pass it:
 // vmcnt retires loads in order, so a bias load issued here would wait for all of them.
-template <int TM, int TN, bool LEAN = false, class RowMap>
+// PLAIN = true (implies LEAN): bias + activations only -- no residual, post-affine or
+// ragged-row mask, i.e. no global load at all.  A persistent kernel with the next tile's
+// loads in flight needs this: a load that may be issued here (even behind a branch the
+// layer never takes) forces waits for everything issued before it (vmcnt counts in order).
+template <int TM, int TN, bool LEAN = false, bool PLAIN = false, class RowMap>
 __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f32x16 (&acc)[TM][TN], int wave,
                                                int lane, int nwave, int M, RowMap rowmap,
                                                const f32x4* pre_bias = nullptr) {
@@ -99,7 +103,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
   constexpr int NTL = TM * TN;
   float amax = 0.f;                            // range guard (common.h)
   if constexpr (NTL <= 2) {
-    if (LEAN || (vec && !part && !d.affx && !d.gate && !d.rowbias)) {
+    if (LEAN || PLAIN || (vec && !part && !d.affx && !d.gate && !d.rowbias)) {
       const int c4 = (lane & 7) * 4;
       f32x4 ra4[NTL][4];
 #pragma unroll
@@ -109,7 +113,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           ra4[tile][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-          if (d.res && n < d.N) {
+          if (!PLAIN && d.res && n < d.N) {
             const int m = max(0, min(rowmap(i * 32 + q * 8 + (lane >> 3)), M - 1));
             ra4[tile][q] = *reinterpret_cast<const f32x4*>(d.res + (size_t)m * d.ldr + n);
           }
@@ -119,12 +123,40 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
       for (int tile = 0; tile < NTL; ++tile) {
         const int i = tile / TN, j = tile % TN;
         const int n = nwave + j * 32 + c4;
+        if constexpr (PLAIN) {
+          // No global load here at all (a load that may be issued, even behind a branch the
+          // layer never takes, makes the compiler wait vmcnt(0) -- for every load issued
+          // before it, i.e. the next tile's prefetch); all four rows are computed first and
+          // stored back to back from distinct registers.
+          const f32x4 bias = pre_bias[tile];
+          const float* ct = cw + tile * 1024;
+          float* const ocol = d.out + n;
+          f32x4 o[4];
+          int mq[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int rl = q * 8 + (lane >> 3);
+            mq[q] = rowmap(i * 32 + rl);
+            o[q] = *reinterpret_cast<const f32x4*>(ct + rl * 32 + c4) + bias;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[q][e] = apply_act(apply_act(o[q][e], d.act), d.act2);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const bool ok = n < d.N && mq[q] >= 0 && mq[q] < M;
+            if (ok) {
+              amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[q][0]), fabsf(o[q][1])), fmaxf(fabsf(o[q][2]), fabsf(o[q][3]))));
+              *reinterpret_cast<f32x4*>(ocol + (size_t)mq[q] * d.ldo) = o[q];
+            }
+          }
+          continue;
+        }
         if (n >= d.N) continue;
         float* const ocol = out_at(d, 0, n);   // plane / column split once per tile, not per row
         f32x4 bias = {0.f, 0.f, 0.f, 0.f}, ps = {1.f, 1.f, 1.f, 1.f}, pt = {0.f, 0.f, 0.f, 0.f};
         if (pre_bias) bias = pre_bias[tile];
         else if (d.bias) bias = *reinterpret_cast<const f32x4*>(d.bias + n);
-        if (d.post_scale) {
+        if (!PLAIN && d.post_scale) {
           ps = *reinterpret_cast<const f32x4*>(d.post_scale + n);
           pt = *reinterpret_cast<const f32x4*>(d.post_shift + n);
         }
@@ -138,10 +170,10 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             float x = apply_act(o[e], d.act);
-            if (d.post_scale) x = x * ps[e] + pt[e];
+            if (!PLAIN && d.post_scale) x = x * ps[e] + pt[e];
             o[e] = apply_act(x, d.act2);
           }
-          if (row_masked(d, m)) o = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (!PLAIN && row_masked(d, m)) o = f32x4{0.f, 0.f, 0.f, 0.f};
           amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
           *reinterpret_cast<f32x4*>(ocol + (size_t)m * d.ldo) = o;
         }
@@ -178,6 +210,26 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
         f32x4 bias = {0.f, 0.f, 0.f, 0.f};
         if (d.bias) bias = *reinterpret_cast<const f32x4*>(d.bias + n);
         const float* ct = cw + tile * 1024;
+        if constexpr (PLAIN) {
+          // all four rows computed first, then four back-to-back stores from distinct
+          // registers: a store whose source registers are reused right away makes the
+          // compiler wait for it (vmcnt(0)), i.e. for every load issued before it
+          f32x4 o[4];
+          int mq[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int rl = q * 8 + (lane >> 3);
+            mq[q] = rowmap(i * 32 + rl);
+            o[q] = *reinterpret_cast<const f32x4*>(ct + rl * 32 + c4) + bias;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[q][e] = apply_act(apply_act(o[q][e], d.act), d.act2);
+            amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[q][0]), fabsf(o[q][1])), fmaxf(fabsf(o[q][2]), fabsf(o[q][3]))));
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (mq[q] >= 0 && mq[q] < M) *reinterpret_cast<f32x4*>(ocol + (size_t)mq[q] * d.ldo) = o[q];
+          continue;
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int rl = q * 8 + (lane >> 3);
@@ -198,7 +250,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
       return;
     }
   }
-  if constexpr (LEAN) return;
+  if constexpr (LEAN || PLAIN) return;
 #pragma unroll 1
   for (int tile = 0; tile < TM * TN; ++tile) {
     {

@@ -241,7 +241,8 @@ class NativeModel:
             _check(lib().spk_model_create(ctypes.byref(c), ws, len(state_dict), ctypes.byref(handle)),
                    'spk_model_create')
         self.handle = handle
-        self._ws: Optional[torch.Tensor] = None
+        self._ws: Optional[torch.Tensor] = None          # workspace of the last forward
+        self._ws_by_stream = {}                           # stream handle -> workspace
         self.last_forward_exact = False
 
     def __del__(self):
@@ -285,15 +286,29 @@ class NativeModel:
             out.append(b.value)
         return out
 
+    def _workspace(self, need: int) -> torch.Tensor:
+        """The calling stream's workspace (grown on demand).  run_graph stages the inputs
+        into the workspace and replays the graph captured for its address, so two forwards
+        in flight on different streams must not share one: each stream gets its own.  A
+        handle is still not safe for concurrent forwards on ONE stream from several threads
+        (they would be serialised on the stream but share the staging space)."""
+        key = _stream(self.device)
+        ws = self._ws_by_stream.get(key)
+        if ws is None or ws.numel() < need:
+            if ws is not None and self._ws is ws:
+                self._ws = None                 # free the old block before the larger one
+            self._ws_by_stream.pop(key, None)
+            ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+            self._ws_by_stream[key] = ws
+        return ws
+
     def forward_timed(self, feats: torch.Tensor, out: torch.Tensor):
         """forward() with a HIP event around every plan step; returns per-step ms."""
         B, T, _ = feats.shape
         n = len(self.plan(B, T))
         ms = (ctypes.c_float * n)()
         with torch.cuda.device(self.device):
-            need = self.workspace_bytes(B, T)
-            if self._ws is None or self._ws.numel() < need:
-                self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+            self._ws = self._workspace(self.workspace_bytes(B, T))
             _check(lib().spk_model_forward_timed(self.handle, feats.data_ptr(), B, T, self._ws.data_ptr(),
                                                  self._ws.numel(), out.data_ptr(), _stream(self.device), ms, n),
                    'spk_model_forward_timed')
@@ -326,9 +341,7 @@ class NativeModel:
                 raise HipError(f'lengths must lie in [{lo}, T={T}] (got min {mn}, max {mx})')
         with torch.cuda.device(self.device):
             need = self.workspace_bytes(B, T) if lengths is None else self.workspace_bytes_lengths(B, T, True)
-            if self._ws is None or self._ws.numel() < need:
-                self._ws = None
-                self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+            self._ws = self._workspace(need)
             if out is None:
                 out = torch.empty((B, self.embed_dim), dtype=torch.float32, device=self.device)
             if lengths is None:

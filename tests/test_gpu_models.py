@@ -148,3 +148,24 @@ def test_out_of_range_lengths_raise(arch, lengths):
     x = torch.zeros(2, 198, 80, device='cuda')
     with pytest.raises((_hip.HipError, ValueError)):
         gpu_module(arch)(x, lengths=torch.tensor(lengths))
+
+
+def test_forward_on_two_streams():
+    """Forwards in flight on two streams get a workspace each (one shared
+    staging / activation space made them overwrite each other); results equal the default
+    stream's, bit for bit (same kernels, same order of reduction)."""
+    g = helpers.golden('eres2netv2')
+    m = gpu_module('eres2netv2')
+    x = [torch.from_numpy(g[f'feats{i}']).cuda() for i in range(2)]
+    with torch.no_grad():
+        ref = [m(xi).clone() for xi in x]
+        s = [torch.cuda.Stream(), torch.cuda.Stream()]
+        out = [None, None]
+        for _ in range(3):
+            for i in range(2):
+                s[i].wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s[i]):
+                    out[i] = m(x[i])
+        torch.cuda.synchronize()
+    for i in range(2):
+        assert torch.equal(out[i], ref[i]), i
