@@ -40,7 +40,11 @@ struct PwCfg {
   static_assert(BM * QR % NT == 0, "A tile must split evenly over the block");
 };
 
-template <int KP, int BN, bool S1>
+// RES (compile time): the layer adds a residual.  Inside the persistent loop every load
+// must be one the compiler can count: a load behind a runtime `d.res ?` (or the ragged-row
+// mask's length load) makes it wait vmcnt(0) -- for the whole two-tile prefetch -- at each
+// use, which serialised the loop (ISA: sixteen such waits per tile).
+template <int KP, int BN, bool S1, bool RES>
 __global__ void __launch_bounds__(512, 1)
 pw_gemm_x3_kernel(const ConvDesc d) {
   using C = PwCfg<KP, BN>;
@@ -128,7 +132,7 @@ pw_gemm_x3_kernel(const ConvDesc d) {
     for (int r = 0; r < 16; ++r) {
       int m = mbase + (r & 3) + 8 * (r >> 2);
       m = m < M ? m : M - 1;
-      res[r] = d.res ? d.res[(size_t)m * d.ldr + (nok ? n : 0)] : 0.f;
+      res[r] = RES ? d.res[(size_t)m * d.ldr + (nok ? n : 0)] : 0.f;
     }
   };
   auto tile = [&](int mt, const float (&res)[16]) {
@@ -156,7 +160,7 @@ pw_gemm_x3_kernel(const ConvDesc d) {
         if (m >= M) continue;
         float v = apply_act(acc[r] + accx[r] * (1.0f / 2048.0f) + bias + res[r], d.act);
         if (d.post_scale) v = v * ps + pt;
-        v = row_masked(d, m) ? 0.f : apply_act(v, d.act2);
+        v = apply_act(v, d.act2);                          // no ragged rows (pw_supported)
         amax = fmaxf(amax, fabsf(v));
         ocol[(size_t)m * d.ldo] = v;
       }
@@ -175,14 +179,17 @@ pw_gemm_x3_kernel(const ConvDesc d) {
   for (int i = 0; i < ntiles; i += 2) {
     float res[16];
     load_res(mt_of(i), res);
-    if (i + 2 < ntiles) load_a(mt_of(i + 2), set0);       // set 0 was staged at the end of i-1
+    __builtin_amdgcn_sched_barrier(0);                    // keep the residual ahead of the prefetch
+    load_a(mt_of(min(i + 2, ntiles - 1)), set0);         // set 0 was staged at the end of i-1;
+                                                          // unconditional (clamped): counted waits
     tile(mt_of(i), res);
     __syncthreads();
     if (i + 1 >= ntiles) break;
     store_a(set1);
     __syncthreads();
     load_res(mt_of(i + 1), res);
-    if (i + 3 < ntiles) load_a(mt_of(i + 3), set1);
+    __builtin_amdgcn_sched_barrier(0);
+    load_a(mt_of(min(i + 3, ntiles - 1)), set1);
     tile(mt_of(i + 1), res);
     __syncthreads();
     if (i + 2 < ntiles) store_a(set0);
@@ -202,14 +209,14 @@ int device_cus_pw() {
   return cached[dev];
 }
 
-template <int KP, int BN, bool S1>
+template <int KP, int BN, bool S1, bool RES>
 hipError_t launch_pw_t(const ConvDesc& d, hipStream_t s) {
   using C = PwCfg<KP, BN>;
   const int M = d.nimg * d.Ho * d.Wo;
   const int nN = (d.N + BN - 1) / BN;
   const int mtiles = (M + C::BM - 1) / C::BM;
   // every resident block slot gets one persistent block owning one N-slice: grid a multiple of nN
-  auto k = pw_gemm_x3_kernel<KP, BN, S1>;
+  auto k = pw_gemm_x3_kernel<KP, BN, S1, RES>;
   static const int per_cu = [&] {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 512, 0) != hipSuccess || n <= 0) n = 1;
@@ -233,14 +240,15 @@ bool pw_supported(const ConvDesc& d) {
                             d.s1.pw == 0 && d.s1.cin % 4 == 0 && d.s1.ld % 4 == 0);
   return d.wh && d.wl && !a.vlen && a.kh == 1 && a.kw == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0 && !a.reflect &&
          !a.pre_scale && !a.p2 && a.ld2 == 0 && s1_ok && (d.Kp == 64 || d.Kp == 128) && d.N <= 256 &&
-         d.N % 4 == 0 && !d.affx && !d.gate && !d.rowbias && d.ksplit == 1 && a.cin % 4 == 0 &&
+         d.N % 4 == 0 && !d.affx && !d.gate && !d.rowbias && !d.rowlen && d.ksplit == 1 && a.cin % 4 == 0 &&
          a.H == d.Ho && a.W == d.Wo && d.nimg * d.Ho * d.Wo >= 65536;
 }
 
 std::string pw_kernel_name(const ConvDesc& d) {
   const bool s1 = d.s1.p != nullptr || d.s1.cin > 0;
+  const bool res = d.res != nullptr || d.ldr > 0;
   return "pw_gemm_x3_kernel<" + std::to_string(d.Kp) + ", " + std::to_string(pw_bn(d)) + ", " +
-         (s1 ? "true" : "false") + ">";
+         (s1 ? "true" : "false") + ", " + (res ? "true" : "false") + ">";
 }
 
 hipError_t launch_pw(const ConvDesc& d, hipStream_t s) {
@@ -248,7 +256,9 @@ hipError_t launch_pw(const ConvDesc& d, hipStream_t s) {
   const bool s1 = d.s1.p != nullptr;
   const int bn = pw_bn(d);
 #define SPK_PW(KP, BNV)                                                         \
-  if (d.Kp == KP && bn == BNV) return s1 ? launch_pw_t<KP, BNV, true>(d, s) : launch_pw_t<KP, BNV, false>(d, s);
+  if (d.Kp == KP && bn == BNV)                                                  \
+    return s1 ? (d.res ? launch_pw_t<KP, BNV, true, true>(d, s) : launch_pw_t<KP, BNV, true, false>(d, s)) \
+              : (d.res ? launch_pw_t<KP, BNV, false, true>(d, s) : launch_pw_t<KP, BNV, false, false>(d, s));
   SPK_PW(64, 64)
   SPK_PW(64, 128)
   SPK_PW(128, 64)
