@@ -413,9 +413,12 @@ res2_block_kernel(const Res2Desc d) {
     }
     // the next tile's first three input chunks, behind the residual (vmcnt retires in order,
     // so the epilogue's wait for the residual does not wait for these)
-    if (t + nslot < t_hi) {
+    // unconditional (the last tile re-reads its own chunks): a load on only some paths
+    // leaves the compiler's wait counts unknown, and the residual waits below became
+    // vmcnt(0), i.e. waits for these chunks too
+    {
       int im, ty0, tx0;
-      tile_origin(t + nslot, im, ty0, tx0);
+      tile_origin(t + nslot < t_hi ? t + nslot : t, im, ty0, tx0);
       const float* pn = d.x + (size_t)im * H * W * CI;
       load_chunk(0, pf[0], ty0, tx0, pn);
       load_chunk(1, pf[1], ty0, tx0, pn);
