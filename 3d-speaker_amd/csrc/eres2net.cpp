@@ -359,21 +359,26 @@ struct ERes2Builder {
       fused = fuse("fuse_mode1234", outs[3], d3);
     }
 
-    // ---- TSTP (pooling_layers.py:47-55) -> stats [B, 2*H*C] in (h, c) order
+    // ---- TSTP (pooling_layers.py:47-55) -> stats [B, 2*H*C] in (h, c) order; TAP / TSDP
+    //      (:10-35, pooling_func) keep only the mean / the std part
+    const int pool = m.cfg.pooling;
+    if (pool < SPK_POOL_TSTP || pool > SPK_POOL_TSDP) throw SpkError(SPK_E_UNSUPPORTED, "pooling must be TSTP, TAP or TSDP");
+    const int parts = pool == SPK_POOL_TAP ? 1 : pool == SPK_POOL_TSDP ? 2 : 3;
+    const int nst = parts == 3 ? 2 : 1;
     const int H4 = fused.H, C4 = fused.C;
-    const int S = 2 * H4 * C4;
+    const int S = nst * H4 * C4;
     const Buf stats = b.alloc((size_t)B * S);
     if (b.plan) {
       const T4 f = fused;
       b.step("pool", [=](const Ctx& c) {
-        return launch_tstp(c.resolve(f.buf), B, f.H, f.W, f.C, f.ld, 1e-8f, 1, c.resolve(stats), c.stream);
+        return launch_tstp(c.resolve(f.buf), B, f.H, f.W, f.C, f.ld, 1e-8f, 1, c.resolve(stats), c.stream, parts);
       });
     }
     // reference flattens (C, F): index c*H + h  -> our h*C + c
     ChanMap perm;
     perm.phys.resize(S);
     perm.n_phys = S;
-    for (int part = 0; part < 2; ++part)
+    for (int part = 0; part < nst; ++part)
       for (int c = 0; c < C4; ++c)
         for (int h = 0; h < H4; ++h) perm.phys[part * H4 * C4 + c * H4 + h] = part * H4 * C4 + h * C4 + c;
     const int E = (int)m.dim("seg_1.weight", 0);

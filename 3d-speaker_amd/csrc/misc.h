@@ -13,7 +13,8 @@ hipError_t launch_range_check(const float* x, size_t n, int* flag, hipStream_t s
 // fp32 -> (hi, lo) fp16 planes for the split-fp16 MFMA GEMM: hi = fp16(w),
 // lo = fp16((w - hi) * 2^11) (conv_gemm.hip, "fp16x3").
 hipError_t launch_split_f16(const float* w, uint16_t* hi, uint16_t* lo, size_t n, hipStream_t s);
+// TSTP / TAP / TSDP (pooling_layers.py:10-55): parts bit 0 = mean, bit 1 = std (TSTP = 3)
 hipError_t launch_tstp(const float* x, int B, int H, int W, int C, int ld, float eps, int unbiased, float* out,
-                       hipStream_t s);
+                       hipStream_t s, int parts = 3);
 
 }  // namespace spk

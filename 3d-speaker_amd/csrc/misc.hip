@@ -76,7 +76,7 @@ __global__ void __launch_bounds__(256) range_check_kernel(const float* __restric
 // x: [B, H, W, C] (pixel stride ld).  out: [B, 2*H*C]: mean at [h*C + c], std at [H*C + h*C + c].
 __global__ void __launch_bounds__(256)
 tstp_kernel(const float* __restrict__ x, int B, int H, int W, int C, int ld, float eps, int unbiased,
-            float* __restrict__ out) {
+            int parts, float* __restrict__ out) {
   const long long total = (long long)B * H * C;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
        e += (long long)gridDim.x * blockDim.x) {
@@ -93,9 +93,11 @@ tstp_kernel(const float* __restrict__ x, int B, int H, int W, int C, int ld, flo
       q = fmaf(dlt, v - mean, q);
     }
     const float var = q / (float)(unbiased ? W - 1 : W);
-    float* o = out + (size_t)b * 2 * H * C;
-    o[h * C + c] = mean;
-    o[H * C + h * C + c] = sqrtf(var + eps);
+    // parts: bit 0 = mean (TAP), bit 1 = std (TSDP); TSTP = both, mean first
+    const int np = (parts & 1) + ((parts >> 1) & 1);
+    float* o = out + (size_t)b * np * H * C;
+    if (parts & 1) o[h * C + c] = mean;
+    if (parts & 2) o[(parts & 1) * H * C + h * C + c] = sqrtf(var + eps);
   }
 }
 
@@ -121,10 +123,11 @@ hipError_t launch_range_check(const float* x, size_t n, int* flag, hipStream_t s
 }
 
 hipError_t launch_tstp(const float* x, int B, int H, int W, int C, int ld, float eps, int unbiased, float* out,
-                       hipStream_t s) {
+                       hipStream_t s, int parts) {
+  if (parts < 1 || parts > 3) return hipErrorInvalidValue;
   const long long total = (long long)B * H * C;
   const int blocks = (int)std::min<long long>((total + 255) / 256, 65536);
-  hipLaunchKernelGGL(tstp_kernel, dim3(blocks), dim3(256), 0, s, x, B, H, W, C, ld, eps, unbiased, out);
+  hipLaunchKernelGGL(tstp_kernel, dim3(blocks), dim3(256), 0, s, x, B, H, W, C, ld, eps, unbiased, parts, out);
   return hipGetLastError();
 }
 

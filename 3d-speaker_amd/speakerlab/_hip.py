@@ -35,7 +35,7 @@ class spk_model_config_t(ctypes.Structure):
                 ('m_channels', ctypes.c_int32), ('base_width', ctypes.c_int32), ('scale', ctypes.c_int32),
                 ('expansion', ctypes.c_int32), ('two_emb_layer', ctypes.c_int32),
                 ('channels', ctypes.c_int32 * 5), ('kernel_sizes', ctypes.c_int32 * 5),
-                ('dilations', ctypes.c_int32 * 5), ('precision', ctypes.c_int32), ('reserved', ctypes.c_int32 * 7)]
+                ('dilations', ctypes.c_int32 * 5), ('precision', ctypes.c_int32), ('pooling', ctypes.c_int32), ('reserved', ctypes.c_int32 * 6)]
 
 
 # spk_model_config_t.precision (include/spk_hip.h)
@@ -215,7 +215,8 @@ class NativeModel:
         c.arch = arch
         c.precision = PRECISIONS[precision]
         self.precision = precision
-        for k in ('feat_dim', 'embed_dim', 'm_channels', 'base_width', 'scale', 'expansion', 'two_emb_layer'):
+        for k in ('feat_dim', 'embed_dim', 'm_channels', 'base_width', 'scale', 'expansion', 'two_emb_layer',
+                  'pooling'):
             setattr(c, k, int(cfg.get(k, 0)))
         for k in ('channels', 'kernel_sizes', 'dilations'):
             vals = list(cfg.get(k, []))[:5]

@@ -14,9 +14,14 @@ no DataLoader workers computing features on the CPU.
 
 Differences forced by the offline environment: weights are read from
 ``<local_model_dir>/<model name>/<model_pt>`` (no modelscope download); ``--synthetic_weights``
-uses deterministic random weights instead (benchmarks / tests).  Non-16 kHz input is
-resampled (the reference's resampling branch raises NameError on ``wav_file`` and skips
-the file, ``infer_sv_batch.py:404-408``).
+uses deterministic random weights instead (benchmarks / tests).
+
+Non-16 kHz input follows the reference's observable behaviour: its resampling branch raises
+NameError on ``wav_file`` (``infer_sv_batch.py:404-405``), the bare ``except`` at ``:361-365``
+catches it, prints the read warning and skips the file -- no embedding is written.
+``--resample_non16k`` (MI355X-build opt-in, off by default) instead resamples such files
+with ``speakerlab.utils.fileio.resample`` (torchaudio's windowed-sinc resampler; the
+reference's intended sox ``rate`` effect is not available here).
 """
 import argparse
 import os
@@ -46,6 +51,8 @@ parser.add_argument('--synthetic_weights', action='store_true',
                     help='MI355X build: deterministic random weights instead of a checkpoint (no network)')
 parser.add_argument('--nprocs', default=None, type=int, help='MI355X build: number of GPU processes')
 parser.add_argument('--io_threads', default=8, type=int, help='MI355X build: wav reader threads per process')
+parser.add_argument('--resample_non16k', action='store_true',
+                    help='MI355X build: resample non-16 kHz wavs (the reference skips them, see module doc)')
 
 
 def _spec(obj, **args):
@@ -104,9 +111,19 @@ def chunk_wav(wav: torch.Tensor, chunk_samples: int):
     return wav.view(n, chunk_samples)
 
 
-def load_wav_chunks(path, obj_fs=SAMPLE_RATE, chunk_size=CHUNK_SECONDS, max_load_len=MAX_LOAD_SECONDS):
-    from speakerlab.utils.fileio import load_audio
-    wav = load_audio(path, obj_fs=obj_fs)[0]
+class SampleRateSkip(Exception):
+    """A non-16 kHz wav: the reference's load_wav fails on it (NameError, :404-405)."""
+
+
+def load_wav_chunks(path, obj_fs=SAMPLE_RATE, chunk_size=CHUNK_SECONDS, max_load_len=MAX_LOAD_SECONDS,
+                    resample_other_rates=False):
+    from speakerlab.utils.fileio import read_wav, resample
+    wav, fs = read_wav(path)
+    if fs != obj_fs:
+        if not resample_other_rates:
+            raise SampleRateSkip(f'sample rate {fs} != {obj_fs}; the reference skips such files')
+        wav = resample(wav, fs, obj_fs)
+    wav = wav.mean(dim=0)
     wav = wav[:int(max_load_len * obj_fs)]
     return chunk_wav(wav, int(chunk_size * obj_fs))
 
@@ -126,7 +143,7 @@ def wav_id_of(path):
     return os.path.basename(path).rsplit('.', 1)[0]
 
 
-def extract(model, wav_paths, batch_size, device, on_result, io_threads=8, progress=None):
+def extract(model, wav_paths, batch_size, device, on_result, io_threads=8, progress=None, resample_other_rates=False):
     """Stream wavs -> chunks -> GPU Fbank + forward -> per-wav mean embedding.
 
     ``on_result(wav_id, embedding[np.float32, E])`` is called in input order."""
@@ -135,7 +152,7 @@ def extract(model, wav_paths, batch_size, device, on_result, io_threads=8, progr
 
     def safe_load(p):
         try:
-            return load_wav_chunks(p)
+            return load_wav_chunks(p, resample_other_rates=resample_other_rates)
         except Exception as e:   # reference: warn and skip unreadable files (:361-365)
             print(f'[WARNING]: Error reading {p}, please check. ({e})')
             return None
@@ -195,7 +212,8 @@ def main_process(rank, nprocs, args, wav_list, conf, local_dir):
     if rank == 0 and not args.diable_progress_bar:
         from tqdm import tqdm
         pbar = tqdm(total=e - s, desc='Processing')
-    extract(model, wav_list[s:e], args.batch_size, device, on_result, args.io_threads, pbar)
+    extract(model, wav_list[s:e], args.batch_size, device, on_result, args.io_threads, pbar,
+            getattr(args, 'resample_non16k', False))
     if pbar is not None:
         pbar.close()
     if writer is not None:

@@ -37,8 +37,8 @@ class ERes2Net(_hip.HipModuleMixin, nn.Module):
     def __init__(self, block=BasicBlockERes2Net, block_fuse=BasicBlockERes2Net_diff_AFF, num_blocks=[3, 4, 6, 3],
                  m_channels=32, feat_dim=80, embedding_size=192, pooling_func='TSTP', two_emb_layer=False):
         super().__init__()
-        if pooling_func != 'TSTP':
-            raise NotImplementedError('the MI355X executor implements TSTP pooling (every registry model uses it)')
+        self.pooling_func = pooling_func
+        pooling_layers.pooling_code(pooling_func)   # TSTP / TAP / TSDP (ASTP raises)
         self.feat_dim, self.embedding_size, self.two_emb_layer = feat_dim, embedding_size, two_emb_layer
         self.m_channels = m_channels
         self.stats_dim = int(feat_dim / 8) * m_channels * 8
@@ -59,15 +59,16 @@ class ERes2Net(_hip.HipModuleMixin, nn.Module):
         self.fuse_mode12 = AFF(channels=m * e * 2)
         self.fuse_mode123 = AFF(channels=m * e * 4)
         self.fuse_mode1234 = AFF(channels=m * e * 8)
-        self.n_stats = 2
-        self.pool = pooling_layers.TSTP(in_dim=self.stats_dim * e)
+        self.n_stats = pooling_layers.n_stats(pooling_func)
+        self.pool = getattr(pooling_layers, pooling_func)(in_dim=self.stats_dim * e)
         embedding_head(self, self.stats_dim * e, self.n_stats, embedding_size, two_emb_layer)
 
     def _hip_config(self):
         b = self._block_cfg
         return dict(feat_dim=self.feat_dim, embed_dim=self.embedding_size, m_channels=self.m_channels,
                     base_width=b['baseWidth'], scale=b['scale'], expansion=b['expansion'],
-                    two_emb_layer=int(bool(self.two_emb_layer)))
+                    two_emb_layer=int(bool(self.two_emb_layer)),
+                    pooling=pooling_layers.pooling_code(self.pooling_func))
 
     def forward(self, x):
         """x: [B, T, feat_dim] float32 on a ROCm device -> [B, embedding_size]."""

@@ -35,8 +35,8 @@ class ERes2NetV2(_hip.HipModuleMixin, nn.Module):
                  m_channels=64, feat_dim=80, embedding_size=192, baseWidth=26, scale=2, expansion=2,
                  pooling_func='TSTP', two_emb_layer=False):
         super().__init__()
-        if pooling_func != 'TSTP':
-            raise NotImplementedError('the MI355X executor implements TSTP pooling (every registry model uses it)')
+        self.pooling_func = pooling_func
+        pooling_layers.pooling_code(pooling_func)   # TSTP / TAP / TSDP (ASTP raises)
         self.feat_dim, self.embedding_size, self.two_emb_layer = feat_dim, embedding_size, two_emb_layer
         self.m_channels, self.baseWidth, self.scale, self.expansion = m_channels, baseWidth, scale, expansion
         self.stats_dim = int(feat_dim / 8) * m_channels * 8
@@ -53,14 +53,15 @@ class ERes2NetV2(_hip.HipModuleMixin, nn.Module):
         self.layer3_ds = nn.Conv2d(m_channels * 4 * expansion, m_channels * 8 * expansion, kernel_size=3, padding=1,
                                    stride=2, bias=False)
         self.fuse34 = AFF(channels=m_channels * 8 * expansion, r=4)
-        self.n_stats = 2
-        self.pool = pooling_layers.TSTP(in_dim=self.stats_dim * expansion)
+        self.n_stats = pooling_layers.n_stats(pooling_func)
+        self.pool = getattr(pooling_layers, pooling_func)(in_dim=self.stats_dim * expansion)
         embedding_head(self, self.stats_dim * expansion, self.n_stats, embedding_size, two_emb_layer)
 
     def _hip_config(self):
         return dict(feat_dim=self.feat_dim, embed_dim=self.embedding_size, m_channels=self.m_channels,
                     base_width=self.baseWidth, scale=self.scale, expansion=self.expansion,
-                    two_emb_layer=int(bool(self.two_emb_layer)))
+                    two_emb_layer=int(bool(self.two_emb_layer)),
+                    pooling=pooling_layers.pooling_code(self.pooling_func))
 
     def forward(self, x):
         """x: [B, T, feat_dim] float32 on a ROCm device -> [B, embedding_size]."""

@@ -5,13 +5,20 @@ One step = the hot path over one batch of synthetic audio already resident in HB
 GPU Kaldi Fbank (80 mel, mean-normalised) of 256 x 32000 samples -> ERes2NetV2 forward
 -> 256 x 192 embeddings.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--with-allgather]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Multi-GPU: utterances shard with no data-path collective (weak scaling: every rank embeds
-its own 256-utterance batches); the barrier + max-over-ranks timing is the only
-communication.  Rank 0 prints ONE JSON line.  The roofline object describes the dominant
+Multi-GPU: one process per GPU.  Under torch.distributed.run the ranks come from the
+environment; a bare `bench.py --gpus N` (N > 1, no WORLD_SIZE) spawns the N rank processes
+itself (spawn context, before this process touches the GPU), the way the reference's
+infer_sv_batch.py:261-280 uses mp.spawn.  Utterances shard with no data-path collective
+(weak scaling: every rank embeds its own 256-utterance batches); the barrier +
+max-over-ranks timing is the only communication, unless --with-allgather adds the C4
+exchange to every step (RCCL all-gather of the step's embeddings from every rank, then this
+rank's row block of the cosine affinity consumed by the top-k kernel,
+speakerlab/utils/distributed.py).  Rank 0 prints ONE JSON line, with the world size the
+process group reports.  The roofline object describes the dominant
 kernel (largest total time inside one forward), measured with HIP events on the stream
 the kernels run on; the CPU baseline is the oracle (op-for-op torch CPU restatement)
 timed on this host on a bounded sample.
@@ -48,7 +55,12 @@ def parse():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--batch', type=int, default=BATCH)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-passes', type=int, default=3, help='timed CPU-baseline passes (best is reported)')
+    ap.add_argument('--cpu-passes', type=int, default=5, help='timed CPU-baseline passes (best is reported)')
+    ap.add_argument('--with-allgather', action='store_true',
+                    help='add the C4 exchange (all-gather of the step embeddings + row-block top-1) to every step')
+    ap.add_argument('--cpu-plumbing', action='store_true',
+                    help='test mode without a GPU: gloo ranks, the step is the exchange on synthetic '
+                         'embeddings only (exercises the launcher and the collectives, measures nothing)')
     ap.add_argument('--traffic-json', default=os.path.join(REPO, 'profiles', 'pmc_traffic.json'),
                     help='per-launch HBM bytes of the dominant kernel from a rocprofv3 --pmc pass (optional)')
     return ap.parse_args()
@@ -190,10 +202,10 @@ def physical_cores():
 
 
 def cpu_baseline(passes, batch=64):
-    """Oracle (op-for-op torch CPU restatement + numpy Fbank) on the host cores: two small
-    warm-up batches, then the best of `passes` timed passes over one batch of `batch`
-    utterances (a bounded sample of the C2 workload: 256-utterance batches would take
-    ~20 s each on 16 cores)."""
+    """Oracle (op-for-op torch CPU restatement + numpy Fbank) on the host cores, SURVEY §8(d):
+    two warm-up passes, then the best of `passes` timed passes over one batch of `batch`
+    utterances (a bounded sample of the C2 workload: a 256-utterance batch takes ~35 s per
+    pass on 16 cores, so the sample is a quarter batch; ~60 s in all)."""
     from oracle import fbank_ref, models_ref
     from speakerlab.utils import synthetic
     from speakerlab.models.eres2net.ERes2NetV2 import ERes2NetV2
@@ -208,7 +220,7 @@ def cpu_baseline(passes, batch=64):
         return models_ref.forward('eres2netv2', sd, feats)
 
     for _ in range(2):
-        one(wavs[:8])
+        one(wavs)
     best = float('inf')
     for _ in range(passes):
         t0 = time.perf_counter()
@@ -216,19 +228,110 @@ def cpu_baseline(passes, batch=64):
         best = min(best, time.perf_counter() - t0)
     return {'value': round(batch / best, 3), 'unit': 'utt/s', 'cores': threads, 'kind': 'port',
             'sample': f'best of {passes} passes over one batch of {batch} utterances of 2 s after 2 warm-up '
-                      f'batches; numpy Fbank + torch CPU fp32 oracle forward, {threads} physical cores '
+                      f'passes over the same batch; numpy Fbank + torch CPU fp32 oracle forward, {threads} physical cores '
                       f'(lscpu, capped at the box\'s 16-CPU share); best pass {best:.2f} s'}
 
 
-def main():
-    args = parse()
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(('127.0.0.1', 0))
+        return so.getsockname()[1]
+
+
+def _rank_entry(rank, world, port, args):
+    """Child process of the self-launcher: the torch.distributed.run environment, then run()."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    run(args)
+
+
+def launch(args):
+    """Spawn args.gpus rank processes (no GPU call in this parent: torch.cuda.device_count()
+    does not initialise the runtime on this image); exit with the worst child status."""
+    import torch.multiprocessing as mp
+    n = args.gpus
+    if not args.cpu_plumbing:
+        have = torch.cuda.device_count()
+        if have < n:
+            raise SystemExit(f'bench.py --gpus {n}: only {have} GPU(s) visible')
+    ctx = mp.get_context('spawn')
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_entry, args=(r, n, port, args)) for r in range(n)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join()
+    bad = [p.exitcode for p in procs if p.exitcode != 0]
+    if bad:
+        raise SystemExit(f'bench.py: rank process(es) failed with exit codes {bad}')
+
+
+def exchange_fn(emb, world, rank, n_total):
+    """C4 exchange on the step's embeddings: the all-gather of every rank's [B, E] block (RCCL
+    all_gather_into_tensor under nccl), then this rank's row block consumed by the top-1
+    cosine kernel (self excluded)."""
+    import torch.distributed as tdist
+    from speakerlab.utils.distributed import all_gather_embeddings, topk_row_block
+    emb_all = all_gather_embeddings(emb, n_total) if tdist.is_initialized() else emb
+    if emb.is_cuda:
+        return topk_row_block(emb_all, rank, world, k=1)
+    return emb_all
+
+
+def plumbing(args, world, rank):
+    """--cpu-plumbing: the launcher + process group + exchange without a GPU (gloo)."""
+    import torch.distributed as tdist
+    B, E = 8, 192
+    g = torch.Generator().manual_seed(rank)
+    emb = torch.randn(B, E, generator=g)
+    for _ in range(args.warmup):
+        exchange_fn(emb, world, rank, B * world)
+    if world > 1:
+        tdist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        got = exchange_fn(emb, world, rank, B * world)
+    if world > 1:
+        tdist.barrier()
+    dt = time.perf_counter() - t0
+    ok = got.shape == (B * world, E) and torch.equal(got[rank * B:(rank + 1) * B], emb)
+    t = torch.tensor([dt])
+    if world > 1:
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    return float(t.item()), B, bool(ok)
+
+
+def run(args):
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     dist = world > 1
+    tdist = None
     if dist:
         import torch.distributed as tdist
-        tdist.init_process_group('nccl' if torch.cuda.is_available() else 'gloo')
+        if args.cpu_plumbing:
+            tdist.init_process_group('gloo')
+        else:
+            dev = torch.device('cuda', local)
+            torch.cuda.set_device(dev)
+            tdist.init_process_group('nccl', device_id=dev)
+        world = tdist.get_world_size()
+    if args.gpus != world and rank == 0:
+        print(f'bench.py: --gpus {args.gpus} but the process group has {world} rank(s); '
+              f'reporting n_gpus = {world}', file=sys.stderr, flush=True)
+
+    if args.cpu_plumbing:
+        dt, B, ok = plumbing(args, world, rank)
+        if rank == 0:
+            print(json.dumps({'metric': METRIC + ' [cpu plumbing test: no GPU work]', 'value': None,
+                              'n_gpus': world, 'world_size': world, 'backend': tdist.get_backend() if dist else None,
+                              'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(dt / args.steps * 1e3, 3),
+                              'exchange_ok': ok, 'rows_per_rank': B}), flush=True)
+        if dist:
+            tdist.destroy_process_group()
+        return
+
     device = torch.device('cuda', local)
     torch.cuda.set_device(device)
 
@@ -241,7 +344,10 @@ def main():
 
     def step():
         feats = _hip.fbank(wavs, 80, mean_nor=True)
-        return model(feats)
+        emb = model(feats)
+        if args.with_allgather:
+            exchange_fn(emb, world, rank, B * world)
+        return emb
 
     with torch.no_grad():
         for _ in range(args.warmup):
@@ -263,6 +369,19 @@ def main():
             t = torch.tensor([dt], device=device)
             tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
             dt = float(t.item())
+        exchange = None
+        if args.with_allgather:
+            # the exchange alone, HIP events on torch's stream (RCCL and the top-k kernel run there)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            reps = 10
+            e0.record()
+            for _ in range(reps):
+                exchange_fn(emb, world, rank, B * world)
+            e1.record()
+            e1.synchronize()
+            exchange = {'ms_per_step': round(e0.elapsed_time(e1) / reps, 4), 'rows_gathered': B * world,
+                        'allgather_bytes': 4 * 192 * B * world,
+                        'what': 'all_gather_embeddings (RCCL) + topk_row_block (spk_cosine_topk, k=1), rank 0'}
         feats = _hip.fbank(wavs, 80, mean_nor=True)
         roof = roofline(model, feats, device, args.traffic_json) if rank == 0 else None
         if roof is not None:
@@ -280,6 +399,8 @@ def main():
             'value': round(value, 2),
             'unit': 'utt/s',
             'n_gpus': world,
+            'world_size': world,
+            'backend': tdist.get_backend() if dist else None,
             'steps': args.steps,
             'warmup': args.warmup,
             'ms_per_step': round(dt / args.steps * 1e3, 3),
@@ -288,17 +409,29 @@ def main():
             'vs_baseline': None,
             'dtype': 'f32 (fp16x3 split-precision MFMA, fp32 accumulate)',
             'data': 'synthetic PCM16 speech-like audio (numpy PCG64), deterministic synthetic weights',
-            'config': {'workload': 'ERes2NetV2 (17.8 M) batch=256 2 s segments, GPU Fbank + embedding, fp32',
+            'config': {'workload': 'ERes2NetV2 (17.8 M) batch=256 2 s segments, GPU Fbank + embedding, fp32'
+                                   + (' + C4 exchange per step' if args.with_allgather else ''),
                        'model': 'ERes2NetV2', 'global_batch': B * world, 'seq_len': 198,
-                       'parallelism': f'dp{world} (utterance sharding, no collective)'},
+                       'parallelism': f'dp{world} (utterance sharding, '
+                                      + ('RCCL all-gather of the embeddings per step)' if args.with_allgather
+                                         else 'no data-path collective)')},
             'model_tflops_achieved': round(value * flops / 1e12, 3),
             'model_gflop_per_utt': round(flops / 1e9, 3),
+            'exchange': exchange,
             'roofline': roof,
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)
     if dist:
         tdist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        launch(args)
+    else:
+        run(args)
 
 
 if __name__ == '__main__':

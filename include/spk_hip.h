@@ -67,6 +67,9 @@ typedef struct {
 /* Constructor arguments of the reference module (only those that shape the graph). */
 #define SPK_PRECISION_FP32 0
 #define SPK_PRECISION_FP16 1
+#define SPK_POOL_TSTP 0
+#define SPK_POOL_TAP 1
+#define SPK_POOL_TSDP 2
 
 typedef struct {
   int32_t arch;
@@ -84,7 +87,9 @@ typedef struct {
                              products); SPK_PRECISION_FP16 (1): one fp16 MFMA product per
                              multiply, fp32 accumulation -- BASELINE config C3's reduced-
                              precision mode (cosine >= 0.9999 to the reference) */
-  int32_t reserved[7];
+  int32_t pooling;        /* ERes2Net*: pooling_func -- SPK_POOL_TSTP (0, default), SPK_POOL_TAP (1),
+                             SPK_POOL_TSDP (2) (pooling_layers.py:10-55); ASTP is not offered */
+  int32_t reserved[6];
 } spk_model_config_t;
 
 int spk_version(void);

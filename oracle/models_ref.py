@@ -81,10 +81,15 @@ def _eres2_block(sd: SD, p: str, x, stride: int, width: int, scale: int, aff: bo
     return _htanh(out + res)
 
 
-def _tstp(x):
-    """TSTP pooling_layers.py:47-55: mean_T, sqrt(var_T(unbiased) + 1e-8), flatten (C,F)."""
+def _tstp(x, pooling='TSTP'):
+    """TSTP pooling_layers.py:47-55: mean_T, sqrt(var_T(unbiased) + 1e-8), flatten (C,F);
+    TAP (:17-21) keeps the mean part, TSDP (:30-35) the std part."""
     mean = x.mean(dim=-1).flatten(start_dim=1)
     std = torch.sqrt(torch.var(x, dim=-1) + 1e-8).flatten(start_dim=1)
+    if pooling == 'TAP':
+        return mean
+    if pooling == 'TSDP':
+        return std
     return torch.cat((mean, std), 1)
 
 
@@ -95,7 +100,7 @@ def _eres2_layer(sd: SD, name: str, x, n_blocks: int, stride: int, width: int, s
 
 
 def eres2netv2_forward(sd: SD, x, m_channels=64, base_width=26, scale=2, num_blocks=(3, 4, 6, 3),
-                       two_emb_layer=False):
+                       two_emb_layer=False, pooling='TSTP'):
     """ERes2NetV2.forward ERes2NetV2.py:235-254. x: [B, T, F]."""
     x = x.permute(0, 2, 1).unsqueeze(1)
     out = F.relu(_bn(F.conv2d(x, sd['conv1.weight'], padding=1), sd, 'bn1'))
@@ -106,7 +111,7 @@ def eres2netv2_forward(sd: SD, x, m_channels=64, base_width=26, scale=2, num_blo
     out4 = _eres2_layer(sd, 'layer4', out3, num_blocks[3], 2, widths[3], scale, True)
     out3_ds = F.conv2d(out3, sd['layer3_ds.weight'], stride=2, padding=1)
     fused = _aff(sd, 'fuse34', out4, out3_ds)
-    emb = F.linear(_tstp(fused), sd['seg_1.weight'], sd['seg_1.bias'])
+    emb = F.linear(_tstp(fused, pooling), sd['seg_1.weight'], sd['seg_1.bias'])
     if two_emb_layer:
         emb = F.linear(_bn(F.relu(emb), sd, 'seg_bn_1'), sd['seg_2.weight'], sd['seg_2.bias'])
     return emb

@@ -162,7 +162,8 @@ hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const fl
 }
 
 hipError_t launch_tstp(const float* x, int B, int H, int W, int C, int ld, float eps, int unbiased, float* out,
-                       hipStream_t) {
+                       hipStream_t, int parts) {
+  const int np = (parts & 1) + ((parts >> 1) & 1);
   for (int b = 0; b < B; ++b)
     for (int h = 0; h < H; ++h)
       for (int c = 0; c < C; ++c) {
@@ -174,8 +175,8 @@ hipError_t launch_tstp(const float* x, int B, int H, int W, int C, int ld, float
           q += dl * dl;
         }
         const double var = q / (unbiased ? W - 1 : W);
-        out[(size_t)b * 2 * H * C + h * C + c] = (float)mean;
-        out[(size_t)b * 2 * H * C + H * C + h * C + c] = (float)std::sqrt(var + eps);
+        if (parts & 1) out[(size_t)b * np * H * C + h * C + c] = (float)mean;
+        if (parts & 2) out[(size_t)b * np * H * C + (parts & 1) * H * C + h * C + c] = (float)std::sqrt(var + eps);
       }
   return hipSuccess;
 }
