@@ -63,10 +63,10 @@ void build_campplus(Builder& b, int T) {
     const int kp = stem.Kp;
     const Buf xo = x.buf;
     const bool rg = b.ragged;
-    int* flag = b.exact ? nullptr : m.range_flag;
+    const bool flag = !b.exact;
     b.step("head.stem", [=](const Ctx& c) {
       return launch_stem_conv3x3(c.in, B, T, F, w, bias, mc, ACT_RELU, kp, c.resolve(xo), mc, c.stream,
-                                 rg ? c.lens : nullptr, flag);
+                                 rg ? c.lens : nullptr, flag ? c.flag : nullptr);
     });
   }
   const ChanMap cm = ChanMap::dense(mc);

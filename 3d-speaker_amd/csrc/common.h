@@ -67,22 +67,33 @@ struct ConvDesc {
   const int* rowlen = nullptr;  // ragged batches: outputs with wo >= rowlen[img] are written as 0
   int* range_flag = nullptr;    // fp16x3 range guard (below): set when an output reaches kRangeLimit
   int x1 = 0;                   // single-product fp16 MFMA (SPK_PRECISION_FP16): hi planes only
+  const int* run_if = nullptr;  // launch gate (below): set by launch_conv from launch_gate()
 };
 
 // fp16x3 range guard.  The split-precision GEMMs represent an operand as two fp16 values,
 // so an activation at or above fp16's largest finite value (65504) would saturate silently.
 // Every producer of an unbounded activation that a split GEMM later reads (conv / linear
-// epilogues, the ERes2Net stem, AFF, the model input) ORs 1 into the handle's flag word when
-// any output it writes reaches 2^15; the ops between two GEMMs grow a value at most 2x
-// (AFF combine, residual + Hardtanh), so below the limit nothing can saturate.  The host
-// reads the flag after the forward and re-runs it on the exact-fp32 kernels when it is set
-// (spk_model_range_check / spk_model_forward_exact).
-constexpr float kRangeLimit = 32768.0f;
+// epilogues, the ERes2Net stem, AFF, the model input) ORs 1 into the forward's range word
+// (a slot of the caller's workspace, zeroed at the start of every forward) when any output
+// it writes reaches kRangeLimit.  The ops between two GEMMs grow a value at most 2x (AFF
+// combine: |x t + y (2 - t)| <= 2 max(|x|, |y|); residual + Hardtanh), so every operand a
+// split GEMM reads stays below 2 kRangeLimit = 2^15 < 65504 (a limit of 2^15 would let a
+// doubled 32767.9 reach 65535.8, past fp16's largest finite value).  The exact-fp32 plan is
+// captured behind the fp16x3 one on the same stream with its launches gated on that word
+// (launch_gate), so a flagged batch is recomputed on the device, without a host round trip.
+constexpr float kRangeLimit = 16384.0f;
 #ifdef __HIPCC__
 __device__ __forceinline__ void range_note(int* flag, float amax) {
   if (flag && amax >= kRangeLimit) atomicOr(flag, 1);
 }
+// launch gate: a kernel of the gated exact plan returns at once unless *run_if != 0 (the
+// word is not written while that plan runs, so every wave of the grid sees the same value)
+#define SPK_GATE(run_if) do { if ((run_if) != nullptr && *(run_if) == 0) return; } while (0)
 #endif
+
+// Host: the gate that launches issued by the calling thread carry (null: ungated).  The
+// plan runner sets it around the exact plan's steps (runtime.cpp GateScope).
+const int* launch_gate();
 
 // XCD-aware bijective block remap: consecutive logical ids (same M tile, all N tiles) are
 // placed on one XCD so the A tile they share stays in that XCD's L2 (the dispatcher deals

@@ -54,6 +54,7 @@ struct HaloCfg {
 template <int CIN, int NP, int PIX, bool ADD>
 __global__ void __launch_bounds__(512, 2)
 conv3x3_halo_kernel(const ConvDesc d, int TW) {
+  SPK_GATE(d.run_if);
   using C = HaloCfg<CIN, NP, PIX, ADD>;
   constexpr int NT = 64 * C::NW;
   __shared__ __attribute__((aligned(16))) float lds[C::LDS];
@@ -188,6 +189,7 @@ struct PersistCfg {
 template <int CIN, int TW, bool ADD>
 __global__ void __launch_bounds__(512, 2)
 conv3x3_halo_persistent_kernel(const ConvDesc d) {
+  SPK_GATE(d.run_if);
   using C = PersistCfg<CIN, ADD>;
   __shared__ __attribute__((aligned(16))) float lds[C::LDS];
   float* halo = lds;
@@ -330,6 +332,7 @@ constexpr int halo_ks(int cin) { return cin > 32 ? 2 : 1; }
 template <int CIN, int TW, bool ADD, int PIX, int KS, bool PLAIN>
 __global__ void __launch_bounds__(64 * (PIX / 32) * KS, 1)
 conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
+  SPK_GATE(d.run_if);
   using C = HaloX3Cfg<CIN, PIX, KS>;
   typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
   typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));

@@ -33,6 +33,7 @@ constexpr int KP_ALIGN = 32;   // weights are packed with Kp a multiple of this
 template <int BM, int BN, int BK, int WM, int WN, bool S1, bool ADD, bool PRE>
 __global__ void __launch_bounds__(64 * WM * WN, 4)
 conv_gemm_kernel(const ConvDesc d) {
+  SPK_GATE(d.run_if);
   constexpr int NT = 64 * WM * WN;               // threads
   constexpr int WTM = BM / WM, WTN = BN / WN;    // wave tile
   constexpr int TM = WTM / 32, TN = WTN / 32;    // 32x32 MFMA tiles per wave
@@ -195,6 +196,7 @@ struct X3Cfg {
 // per product, fp32 accumulation; only the hi planes are staged.
 template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE, bool BUF, bool X1>
 __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
+  SPK_GATE(d.run_if);
   using C = X3Cfg<BM, BN, WM, WN, X1>;
   constexpr int BK = C::BK, TM = C::TM, TN = C::TN, RPP = C::RPP, AROWS = C::AROWS;
   static_assert(TM >= 1 && TN >= 1 && BM % RPP == 0, "tile shape");
@@ -366,6 +368,7 @@ conv_gemm_x1_kernel(const ConvDesc d) {
 
 // Split-K combine: out = epi(sum_z partial[z])   (fixed z order: deterministic)
 __global__ void splitk_reduce_kernel(const ConvDesc d, int M) {
+  SPK_GATE(d.run_if);
   const size_t total = (size_t)M * d.N;
   float amax = 0.f;
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
@@ -509,7 +512,9 @@ int conv_tile_blocks(const ConvDesc& d) {
 
 bool conv_use_x3() { return use_x3(); }
 
-hipError_t launch_conv(const ConvDesc& d, hipStream_t s) {
+hipError_t launch_conv(const ConvDesc& dd, hipStream_t s) {
+  ConvDesc d = dd;
+  d.run_if = launch_gate();
   // host-side shape checks: every float4 access must stay aligned and in range
   if (d.s0.cin % 4 || d.s0.ld % 4 || (d.s0.p2 && d.s0.ld2 % 4) || d.Kp % KP_ALIGN || (d.osplit ? (d.osplit % 4 || d.ldo < d.osplit) : d.ldo < d.N) ||
       (d.s1.p && (d.s1.cin % 4 || d.s1.ld % 4)) || d.N <= 0 || d.nimg <= 0 || d.Ho <= 0 || d.Wo <= 0 ||

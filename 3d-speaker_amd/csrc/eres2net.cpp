@@ -100,7 +100,6 @@ struct ERes2Builder {
       ad.b1 = m.dptr(a0.b_off); ad.kp1 = a0.Kp;
       ad.w2 = m.dptr(a1.w_off); ad.w2h = m.dhi(a1.w_off); ad.w2l = m.dlo(a1.w_off);
       ad.b2 = m.dptr(a1.b_off); ad.kp2 = a1.Kp;
-      ad.range_flag = m.range_flag;
       if (!a0.has_bias || !a1.has_bias) throw SpkError(SPK_E_WEIGHTS, p + ": AFF convs without bias");
       const double bytes = 4.0 * ad.M * (3.0 * C) + 4.0 * ((double)a0.N * a0.K + (double)a1.N * a1.K);
       const Buf xb = x.buf, yb = y.buf, ob = out.buf;
@@ -108,6 +107,7 @@ struct ERes2Builder {
         ad.x = c.resolve(xb);
         ad.y = c.resolve(yb);
         ad.out = c.resolve(ob);
+        ad.range_flag = c.flag;
         return launch_aff_x3(ad, c.stream);
       }, aff_x3_kernel_name(mid.n_phys), bytes);
       return;
@@ -282,9 +282,9 @@ struct ERes2Builder {
       const int kp = stem.Kp;
       const Buf xo = x.buf;
       const int ld = x.ld;
-      int* flag = b.exact ? nullptr : m.range_flag;
+      const bool flag = !b.exact;
       b.step("stem", [=](const Ctx& c) {
-        return launch_stem_conv3x3(c.in, B, T, F, w, bias, mc, ACT_RELU, kp, c.resolve(xo), ld, c.stream, nullptr, flag);
+        return launch_stem_conv3x3(c.in, B, T, F, w, bias, mc, ACT_RELU, kp, c.resolve(xo), ld, c.stream, nullptr, flag ? c.flag : nullptr);
       });
     }
     // ---- scratch for the block internals, sized by the largest layer

@@ -8,6 +8,8 @@ namespace spk {
 hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const float* w, const float* bias, int cout,
                                int act, int wstride, float* out, int ldo, hipStream_t s, const int* vlen = nullptr,
                                int* range_flag = nullptr);
+// range word of a forward := 0 (a kernel node, not a memset node, in the captured forward)
+hipError_t launch_word_reset(int* w, hipStream_t s);
 // range guard on a model input (common.h kRangeLimit): flag |= 1 if any |x[i]| >= 2^15
 hipError_t launch_range_check(const float* x, size_t n, int* flag, hipStream_t s);
 // fp32 -> (hi, lo) fp16 planes for the split-fp16 MFMA GEMM: hi = fp16(w),

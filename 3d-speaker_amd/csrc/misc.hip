@@ -16,7 +16,8 @@ namespace {
 __global__ void __launch_bounds__(256)
 stem_conv3x3_kernel(const float* __restrict__ feats, int B, int T, int F, const float* __restrict__ w,
                     const float* __restrict__ bias, int cout, int act, int wstride, float* __restrict__ out,
-                    int ldo, const int* __restrict__ vlen, int* range_flag) {
+                    int ldo, const int* __restrict__ vlen, int* range_flag, const int* __restrict__ run_if) {
+  SPK_GATE(run_if);
   // thread -> (pixel, 16 output channels); pixel = (b, f, t) of the (F, T) image.  Weights and
   // bias are staged in LDS once per block; 32-bit index math only.
   __shared__ float ws[128 * 9];
@@ -76,7 +77,8 @@ __global__ void __launch_bounds__(256) range_check_kernel(const float* __restric
 // x: [B, H, W, C] (pixel stride ld).  out: [B, 2*H*C]: mean at [h*C + c], std at [H*C + h*C + c].
 __global__ void __launch_bounds__(256)
 tstp_kernel(const float* __restrict__ x, int B, int H, int W, int C, int ld, float eps, int unbiased,
-            int parts, float* __restrict__ out) {
+            int parts, float* __restrict__ out, const int* __restrict__ run_if) {
+  SPK_GATE(run_if);
   const long long total = (long long)B * H * C;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
        e += (long long)gridDim.x * blockDim.x) {
@@ -111,7 +113,7 @@ hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const fl
   const long long total = (long long)B * F * T * (cout / 16);
   const int blocks = (int)std::min<long long>((total + 255) / 256, 65536);
   hipLaunchKernelGGL(stem_conv3x3_kernel, dim3(blocks), dim3(256), 0, s, feats, B, T, F, w, bias, cout, act, wstride, out,
-                     ldo, vlen, range_flag);
+                     ldo, vlen, range_flag, launch_gate());
   return hipGetLastError();
 }
 
@@ -127,7 +129,16 @@ hipError_t launch_tstp(const float* x, int B, int H, int W, int C, int ld, float
   if (parts < 1 || parts > 3) return hipErrorInvalidValue;
   const long long total = (long long)B * H * C;
   const int blocks = (int)std::min<long long>((total + 255) / 256, 65536);
-  hipLaunchKernelGGL(tstp_kernel, dim3(blocks), dim3(256), 0, s, x, B, H, W, C, ld, eps, unbiased, parts, out);
+  hipLaunchKernelGGL(tstp_kernel, dim3(blocks), dim3(256), 0, s, x, B, H, W, C, ld, eps, unbiased, parts, out, launch_gate());
+  return hipGetLastError();
+}
+
+__global__ void word_reset_kernel(int* w) {
+  if (threadIdx.x == 0) *w = 0;
+}
+
+hipError_t launch_word_reset(int* w, hipStream_t s) {
+  hipLaunchKernelGGL(word_reset_kernel, dim3(1), dim3(64), 0, s, w);
   return hipGetLastError();
 }
 

@@ -16,6 +16,7 @@
 // conflict-free ds_read_b128).  Epilogue straight from the MFMA C layout (lane = column):
 // each store instruction writes two full 128-B row segments.
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 
 #include "common.h"
@@ -47,6 +48,7 @@ struct PwCfg {
 template <int KP, int BN, bool S1, bool RES>
 __global__ void __launch_bounds__(512, 1)
 pw_gemm_x3_kernel(const ConvDesc d) {
+  SPK_GATE(d.run_if);
   using C = PwCfg<KP, BN>;
   __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
   _Float16* Bh = reinterpret_cast<_Float16*>(lds);
@@ -233,6 +235,8 @@ int pw_bn(const ConvDesc& d) { return d.N <= 64 ? 64 : 128; }
 }  // namespace
 
 bool pw_supported(const ConvDesc& d) {
+  static const bool off = std::getenv("SPK_NO_PW") != nullptr;   // diagnostics: implicit GEMM instead
+  if (off) return false;
   const ConvSrc& a = d.s0;
   const bool s1_ok = !d.s1.p && d.s1.cin == 0
                          ? true

@@ -185,9 +185,9 @@ struct ResBuilder {
       const float* bias = m.dptr(stem.b_off);
       const int kp = stem.Kp;
       const Buf xo = x.buf;
-      int* flag = b.exact ? nullptr : m.range_flag;
+      const bool flag = !b.exact;
       b.step("stem", [=](const Ctx& c) {
-        return launch_stem_conv3x3(c.in, B, T, F, w, bias, mc, ACT_RELU, kp, c.resolve(xo), mc, c.stream, nullptr, flag);
+        return launch_stem_conv3x3(c.in, B, T, F, w, bias, mc, ACT_RELU, kp, c.resolve(xo), mc, c.stream, nullptr, flag ? c.flag : nullptr);
       });
     }
     // ---- block scratch sized by the largest stage

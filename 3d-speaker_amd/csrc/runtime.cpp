@@ -11,8 +11,18 @@
 namespace spk {
 
 thread_local std::string g_last_error;
+thread_local const int* g_launch_gate = nullptr;
 
 void set_error(const std::string& msg) { g_last_error = msg; }
+
+const int* launch_gate() { return g_launch_gate; }
+
+// launches issued in this scope carry `gate` (common.h SPK_GATE)
+struct GateScope {
+  const int* prev;
+  explicit GateScope(const int* g) : prev(g_launch_gate) { g_launch_gate = g; }
+  ~GateScope() { g_launch_gate = prev; }
+};
 
 ChanMap ChanMap::dense(int c, int align) {
   ChanMap m;
@@ -118,7 +128,8 @@ const Packed& Model::pack(const std::string& name, const ChanMap& out, const std
   Packed p;
   p.N = N; p.K = K; p.Kp = Kp; p.has_bias = has_bias;
   std::vector<float> wf(wd.begin(), wd.end()), bf(bd.begin(), bd.end());
-  for (float v : wf) gemm_wmax = std::max(gemm_wmax, std::fabs(v));   // range guard (common.h)
+  for (float v : wf) p.wmax = std::max(p.wmax, std::fabs(v));
+  gemm_wmax = std::max(gemm_wmax, p.wmax);   // range guard (common.h)
   p.w_off = put(wf);
   p.b_off = put(bf);
   return packed.emplace(name, p).first->second;
@@ -164,7 +175,7 @@ void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const C
   d.w = m.dptr(p.w_off);
   d.wh = exact ? nullptr : m.dhi(p.w_off);   // no split planes: the exact-fp32 kernels are chosen
   d.wl = exact ? nullptr : m.dlo(p.w_off);
-  d.range_flag = exact ? nullptr : m.range_flag;
+  const bool guard = !exact;   // producers note fp16x3 range overflows in the forward's word
   d.x1 = (!exact && m.fp16 && x1_scope) ? 1 : 0;
   d.bias = (use_bias && p.has_bias) ? m.dptr(p.b_off) : nullptr;
   const int M = d.nimg * d.Ho * d.Wo;
@@ -194,7 +205,8 @@ void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const C
   if (io.s1) bytes += 4.0 * px_out * d.s1.cin;
   if (io.res) bytes += 4.0 * px_out * d.N;
   if (io.affx) bytes += 8.0 * px_out * d.N;
-  step(name, [d, cio](const Ctx& c) mutable {
+  step(name, [d, cio, guard](const Ctx& c) mutable {
+    d.range_flag = guard ? c.flag : nullptr;
     d.s0.p = c.resolve(cio.s0);
     d.s0.p2 = c.resolve(cio.s0b);
     d.s1.p = c.resolve(cio.s1);
@@ -248,37 +260,22 @@ int hip_check(hipError_t e, const char* what) {
 
 }  // namespace
 
-spk::Plan::~Plan() {
+spk::PlanPair::~PlanPair() {
+  // an evicted pair is destroyed by the last forward holding it, after that forward has
+  // enqueued its graph: wait for the device before the executable graphs go
+  if (!graphs.empty()) (void)hipDeviceSynchronize();
   for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
 }
 
 namespace {
 
-Plan* get_plan(spk_model_t* h, int B, int T, bool ragged = false, bool exact = false) {
-  std::lock_guard<std::mutex> lk(h->m.mu);
-  exact = exact || h->m.force_exact || !conv_use_x3();
-  const auto key = std::make_tuple(B, T, (int)ragged, (int)exact);
-  h->m.plan_use[key] = ++h->m.plan_clock;
-  auto it = h->m.plans.find(key);
-  if (it != h->m.plans.end()) return it->second.get();
-  if (ragged && h->m.cfg.arch != SPK_ARCH_CAMPPLUS && h->m.cfg.arch != SPK_ARCH_ECAPA)
-    throw SpkError(SPK_E_UNSUPPORTED, "per-utterance lengths are implemented for CAM++ and ECAPA-TDNN only");
-  if (h->m.plans.size() >= Model::kMaxPlans) {
-    // evict the least recently used plan; its graphs may still run on some stream
-    auto victim = h->m.plans.begin();
-    for (auto p = h->m.plans.begin(); p != h->m.plans.end(); ++p)
-      if (h->m.plan_use[p->first] < h->m.plan_use[victim->first]) victim = p;
-    (void)hipDeviceSynchronize();
-    h->m.plan_use.erase(victim->first);
-    h->m.plans.erase(victim);
-  }
+std::unique_ptr<Plan> build_plan(spk_model_t* h, int B, int T, bool ragged, bool exact) {
   auto plan = std::make_unique<Plan>();
   Builder b(h->m, plan.get(), B, ragged, exact);
   if (!exact) {
     // fp16x3 range guard on the model input (common.h)
     const size_t n = (size_t)B * T * h->m.cfg.feat_dim;
-    int* flag = h->m.range_flag;
-    b.step("range_in", [n, flag](const Ctx& c) { return launch_range_check(c.in, n, flag, c.stream); });
+    b.step("range_in", [n](const Ctx& c) { return launch_range_check(c.in, n, c.flag, c.stream); });
   }
   switch (h->m.cfg.arch) {
     case SPK_ARCH_ERES2NETV2: build_eres2net(b, T, true); break;
@@ -289,22 +286,51 @@ Plan* get_plan(spk_model_t* h, int B, int T, bool ragged = false, bool exact = f
     case SPK_ARCH_RES2NET: build_resnet(b, T, true); break;
     default: throw SpkError(SPK_E_UNSUPPORTED, "unknown arch");
   }
-  // staging regions for graph replay (input features, per-utterance lengths, embeddings)
-  plan->in_bytes = (size_t)B * T * h->m.cfg.feat_dim * sizeof(float);
-  plan->out_bytes = (size_t)B * h->m.cfg.embed_dim * sizeof(float);
-  plan->len_bytes = ragged ? (size_t)B * sizeof(int32_t) : 0;
-  size_t ws = (b.ws + 255) / 256 * 256;
-  plan->stage_in = ws;
-  ws += (plan->in_bytes + 255) / 256 * 256;
-  plan->stage_out = ws;
-  ws += (plan->out_bytes + 255) / 256 * 256;
-  plan->stage_len = ws;
-  ws += (plan->len_bytes + 255) / 256 * 256;
-  plan->ws_bytes = ws;
-  Plan* p = plan.get();
-  h->m.plans.emplace(key, std::move(plan));
-  return p;
+  plan->ws_bytes = (b.ws + 255) / 256 * 256;
+  return plan;
 }
+
+std::shared_ptr<PlanPair> get_pair(spk_model_t* h, int B, int T, bool ragged = false) {
+  std::lock_guard<std::mutex> lk(h->m.mu);
+  const bool exact_only = h->m.force_exact || !conv_use_x3();
+  const auto key = std::make_tuple(B, T, (int)ragged);
+  h->m.plan_use[key] = ++h->m.plan_clock;
+  auto it = h->m.plans.find(key);
+  if (it != h->m.plans.end()) return it->second;
+  if (ragged && h->m.cfg.arch != SPK_ARCH_CAMPPLUS && h->m.cfg.arch != SPK_ARCH_ECAPA)
+    throw SpkError(SPK_E_UNSUPPORTED, "per-utterance lengths are implemented for CAM++ and ECAPA-TDNN only");
+  if (h->m.plans.size() >= Model::kMaxPlans) {
+    // evict the least recently used pair: forwards still holding it keep it alive
+    auto victim = h->m.plans.begin();
+    for (auto p = h->m.plans.begin(); p != h->m.plans.end(); ++p)
+      if (h->m.plan_use[p->first] < h->m.plan_use[victim->first]) victim = p;
+    h->m.plan_use.erase(victim->first);
+    h->m.plans.erase(victim);
+  }
+  auto pair = std::make_shared<PlanPair>();
+  if (!exact_only) pair->x3 = build_plan(h, B, T, ragged, false);
+  pair->ex = build_plan(h, B, T, ragged, true);
+  // shared layout: intermediates, then staging (input features, lengths, embeddings) and the
+  // range word, all past both plans' intermediates
+  size_t ws = std::max(pair->x3 ? pair->x3->ws_bytes : 0, pair->ex->ws_bytes);
+  pair->in_bytes = (size_t)B * T * h->m.cfg.feat_dim * sizeof(float);
+  pair->out_bytes = (size_t)B * h->m.cfg.embed_dim * sizeof(float);
+  pair->len_bytes = ragged ? (size_t)B * sizeof(int32_t) : 0;
+  pair->stage_in = ws;
+  ws += (pair->in_bytes + 255) / 256 * 256;
+  pair->stage_out = ws;
+  ws += (pair->out_bytes + 255) / 256 * 256;
+  pair->stage_len = ws;
+  ws += (pair->len_bytes + 255) / 256 * 256;
+  pair->stage_flag = ws;
+  ws += 256;
+  pair->ws_bytes = ws;
+  h->m.plans.emplace(key, pair);
+  return pair;
+}
+
+// the plan a measurement / introspection call describes: the fp16x3 one unless exact only
+Plan* main_plan(const std::shared_ptr<PlanPair>& p) { return p->x3 ? p->x3.get() : p->ex.get(); }
 
 }  // namespace
 
@@ -429,16 +455,15 @@ int spk_model_create(const spk_model_config_t* cfg, const spk_weight_t* weights,
         (void)hipFree(h->m.dweights);
         return rc;
       }
-      if (int rc = hip_check(launch_split_f16(h->m.dweights, h->m.dsplit, h->m.dsplit + n, n, nullptr), "split_f16"))
+      if (int rc = hip_check(launch_split_f16(h->m.dweights, h->m.dsplit, h->m.dsplit + n, n, nullptr),
+                             "split_f16"))
         return rc;
       if (int rc = hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize")) return rc;
     }
     {
-      // fp16x3 range guard (common.h): a weight past fp16's range forces the exact path;
-      // the activation flag word is cleared once here and by spk_model_range_check
+      // fp16x3 range guard (common.h): a weight past fp16's range forces the exact path
+      // (the activations' range word lives in each forward's workspace)
       h->m.force_exact = !(h->m.gemm_wmax < 65504.0f);   // the split GEMM operands only
-      if (int rc = hip_check(hipMalloc(&h->m.range_flag, 256), "hipMalloc(range flag)")) return rc;
-      if (int rc = hip_check(hipMemset(h->m.range_flag, 0, 256), "hipMemset(range flag)")) return rc;
     }
     h->m.uploaded = true;
     h->m.arena.clear();
@@ -453,7 +478,6 @@ int spk_model_destroy(spk_model_t* model) {
   if (!model) return SPK_OK;
   if (model->m.dweights) (void)hipFree(model->m.dweights);
   if (model->m.dsplit) (void)hipFree(model->m.dsplit);
-  if (model->m.range_flag) (void)hipFree(model->m.range_flag);
   delete model;
   return SPK_OK;
 }
@@ -464,7 +488,7 @@ int spk_model_workspace_bytes(spk_model_t* model, int32_t B, int32_t T, size_t* 
       set_error("spk_model_workspace_bytes: invalid argument");
       return SPK_E_INVALID;
     }
-    *bytes = std::max(get_plan(model, B, T)->ws_bytes, get_plan(model, B, T, false, true)->ws_bytes);
+    *bytes = get_pair(model, B, T)->ws_bytes;
     return SPK_OK;
   });
 }
@@ -499,26 +523,56 @@ static bool use_graphs() {
   return on;
 }
 
-// Replay the plan as one hipGraph: inputs are copied into the workspace's staging regions,
+// Enqueue one forward: the range word is zeroed, the fp16x3 plan runs (its producers note
+// range overflows in the word), then the exact-fp32 plan runs with every launch gated on the
+// word (common.h SPK_GATE): a batch whose activations left fp16's range is recomputed on the
+// exact kernels and overwrites the embeddings, all on `stream`, with no host round trip.
+// `exact` runs the exact plan alone (spk_model_forward_exact).
+static int enqueue_steps(const char* fn, const PlanPair& pp, const Ctx& base, bool exact) {
+  auto run = [&](const Plan& p, int* flag, const int* gate) -> int {
+    Ctx c = base;
+    c.flag = flag;
+    GateScope g(gate);
+    for (size_t i = 0; i < p.steps.size(); ++i) {
+      hipError_t e = p.steps[i](c);
+      if (e != hipSuccess) {
+        set_error(std::string(fn) + ": step '" + p.names[i] + "': " + hipGetErrorString(e));
+        return SPK_E_HIP;
+      }
+    }
+    return SPK_OK;
+  };
+  if (exact || !pp.x3) return run(*pp.ex, nullptr, nullptr);
+  int* word = reinterpret_cast<int*>(base.ws + pp.stage_flag);
+  if (int rc = hip_check(launch_word_reset(word, base.stream), "range word reset")) return rc;
+  if (int rc = run(*pp.x3, word, nullptr)) return rc;
+  static const bool no_rerun = std::getenv("SPK_DIAG_NO_RERUN") != nullptr;   // diagnostics only
+  if (no_rerun) return SPK_OK;
+  return run(*pp.ex, nullptr, word);
+}
+
+// Replay the forward as one hipGraph: inputs are copied into the workspace's staging regions,
 // the graph (captured once per workspace address on a private stream) runs on the caller's
 // stream, and the embeddings are copied out.  Removes the per-kernel launch cost (CAM++ has
 // ~280 launches per forward).
-static int run_graph(const char* fn, spk_model_t* model, Plan* plan, const float* feats, const int32_t* lengths,
-                     char* ws, float* emb_out, hipStream_t stream) {
-  char* in_s = ws + plan->stage_in;
-  char* out_s = ws + plan->stage_out;
-  char* len_s = ws + plan->stage_len;
-  if (int rc = hip_check(hipMemcpyAsync(in_s, feats, plan->in_bytes, hipMemcpyDeviceToDevice, stream), "stage in"))
+static int run_graph(const char* fn, spk_model_t* model, PlanPair& pp, const float* feats, const int32_t* lengths,
+                     char* ws, float* emb_out, hipStream_t stream, bool exact) {
+  char* in_s = ws + pp.stage_in;
+  char* out_s = ws + pp.stage_out;
+  char* len_s = ws + pp.stage_len;
+  if (int rc = hip_check(hipMemcpyAsync(in_s, feats, pp.in_bytes, hipMemcpyDeviceToDevice, stream), "stage in"))
     return rc;
-  if (lengths && plan->len_bytes)
-    if (int rc = hip_check(hipMemcpyAsync(len_s, lengths, plan->len_bytes, hipMemcpyDeviceToDevice, stream),
+  if (lengths && pp.len_bytes)
+    if (int rc = hip_check(hipMemcpyAsync(len_s, lengths, pp.len_bytes, hipMemcpyDeviceToDevice, stream),
                            "stage lengths"))
       return rc;
+  // the exact-only replay (spk_model_forward_exact) is keyed apart from the guarded one
+  const void* key = exact ? static_cast<const void*>(ws + 1) : static_cast<const void*>(ws);
   hipGraphExec_t exec = nullptr;
   {
     std::lock_guard<std::mutex> lk(model->m.mu);
-    auto it = plan->graphs.find(ws);
-    if (it != plan->graphs.end()) exec = it->second;
+    auto it = pp.graphs.find(key);
+    if (it != pp.graphs.end()) exec = it->second;
   }
   if (!exec) {
     hipStream_t cap = nullptr;
@@ -527,13 +581,7 @@ static int run_graph(const char* fn, spk_model_t* model, Plan* plan, const float
           lengths ? reinterpret_cast<const int*>(len_s) : nullptr};
     hipGraph_t graph = nullptr;
     int rc = hip_check(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
-    for (size_t i = 0; rc == SPK_OK && i < plan->steps.size(); ++i) {
-      hipError_t e = plan->steps[i](c);
-      if (e != hipSuccess) {
-        set_error(std::string(fn) + ": capture of step '" + plan->names[i] + "': " + hipGetErrorString(e));
-        rc = SPK_E_HIP;
-      }
-    }
+    if (rc == SPK_OK) rc = enqueue_steps(fn, pp, c, exact);
     const hipError_t ee = hipStreamEndCapture(cap, &graph);
     if (rc == SPK_OK) rc = hip_check(ee, "hipStreamEndCapture");
     if (rc == SPK_OK) rc = hip_check(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0), "hipGraphInstantiate");
@@ -541,14 +589,14 @@ static int run_graph(const char* fn, spk_model_t* model, Plan* plan, const float
     (void)hipStreamDestroy(cap);
     if (rc != SPK_OK) return rc;
     std::lock_guard<std::mutex> lk(model->m.mu);
-    auto ins = plan->graphs.emplace(ws, exec);
+    auto ins = pp.graphs.emplace(key, exec);
     if (!ins.second) {   // another thread captured the same one first
       (void)hipGraphExecDestroy(exec);
       exec = ins.first->second;
     }
   }
   if (int rc = hip_check(hipGraphLaunch(exec, stream), "hipGraphLaunch")) return rc;
-  return hip_check(hipMemcpyAsync(emb_out, out_s, plan->out_bytes, hipMemcpyDeviceToDevice, stream), "stage out");
+  return hip_check(hipMemcpyAsync(emb_out, out_s, pp.out_bytes, hipMemcpyDeviceToDevice, stream), "stage out");
 }
 
 static int run_forward(const char* fn, spk_model_t* model, const float* feats, int32_t B, int32_t T,
@@ -564,23 +612,16 @@ static int run_forward(const char* fn, spk_model_t* model, const float* feats, i
     set_error(std::string(fn) + ": handle belongs to another device");
     return SPK_E_DEVICE;
   }
-  Plan* plan = get_plan(model, B, T, lengths != nullptr, exact);
-  if (workspace_bytes < plan->ws_bytes || (plan->ws_bytes && !workspace)) {
-    set_error(std::string(fn) + ": workspace too small (need " + std::to_string(plan->ws_bytes) + " bytes)");
+  const std::shared_ptr<PlanPair> pp = get_pair(model, B, T, lengths != nullptr);
+  if (workspace_bytes < pp->ws_bytes || !workspace) {
+    set_error(std::string(fn) + ": workspace too small (need " + std::to_string(pp->ws_bytes) + " bytes)");
     return SPK_E_WORKSPACE;
   }
+  const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (use_graphs())
-    return run_graph(fn, model, plan, feats, lengths, reinterpret_cast<char*>(workspace), emb_out,
-                     reinterpret_cast<hipStream_t>(stream));
-  Ctx c{reinterpret_cast<char*>(workspace), feats, emb_out, reinterpret_cast<hipStream_t>(stream), lengths};
-  for (size_t i = 0; i < plan->steps.size(); ++i) {
-    hipError_t e = plan->steps[i](c);
-    if (e != hipSuccess) {
-      set_error(std::string(fn) + ": step '" + plan->names[i] + "': " + hipGetErrorString(e));
-      return SPK_E_HIP;
-    }
-  }
-  return SPK_OK;
+    return run_graph(fn, model, *pp, feats, lengths, reinterpret_cast<char*>(workspace), emb_out, s, exact);
+  Ctx c{reinterpret_cast<char*>(workspace), feats, emb_out, s, lengths};
+  return enqueue_steps(fn, *pp, c, exact);
 }
 
 int spk_model_forward(spk_model_t* model, const float* feats, int32_t B, int32_t T, void* workspace,
@@ -596,7 +637,7 @@ int spk_model_workspace_bytes_lengths(spk_model_t* model, int32_t B, int32_t T, 
       set_error("spk_model_workspace_bytes_lengths: invalid argument");
       return SPK_E_INVALID;
     }
-    *bytes = std::max(get_plan(model, B, T, ragged != 0)->ws_bytes, get_plan(model, B, T, ragged != 0, true)->ws_bytes);
+    *bytes = get_pair(model, B, T, ragged != 0)->ws_bytes;
     return SPK_OK;
   });
 }
@@ -617,20 +658,45 @@ int spk_model_forward_exact(spk_model_t* model, const float* feats, int32_t B, i
   });
 }
 
-int spk_model_range_check(spk_model_t* model, void* stream, int32_t* overflowed) {
+int spk_model_range_check(spk_model_t* model, int32_t B, int32_t T, int32_t ragged, const void* workspace,
+                          void* stream, int32_t* overflowed) {
   return guarded([&]() -> int {
-    if (!model || !overflowed || !model->m.range_flag) {
+    if (!model || !overflowed || !workspace || B <= 0 || T <= 0) {
       set_error("spk_model_range_check: invalid argument");
       return SPK_E_INVALID;
     }
+    const auto pp = get_pair(model, B, T, ragged != 0);
+    *overflowed = 0;
+    if (!pp->x3) return SPK_OK;   // exact-only handle: nothing is guarded
     const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int v = 0;
-    if (int rc = hip_check(hipMemcpyAsync(&v, model->m.range_flag, sizeof(int), hipMemcpyDeviceToHost, s), "range flag"))
-      return rc;
+    const char* word = reinterpret_cast<const char*>(workspace) + pp->stage_flag;
+    if (int rc = hip_check(hipMemcpyAsync(&v, word, sizeof(int), hipMemcpyDeviceToHost, s), "range word")) return rc;
     if (int rc = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize")) return rc;
-    if (v)
-      if (int rc = hip_check(hipMemsetAsync(model->m.range_flag, 0, sizeof(int), s), "range flag reset")) return rc;
     *overflowed = v != 0;
+    return SPK_OK;
+  });
+}
+
+// Diagnostics (tools/race_probe*.py; not in include/spk_hip.h): run the first `nsteps` steps
+// of the fp16x3 (exact = 0) or exact (exact = 1) plan directly on `stream`, the range word
+// being the workspace slot of a guarded forward (not reset here).
+int spk_diag_run_prefix(spk_model_t* model, const float* feats, int32_t B, int32_t T, void* workspace,
+                        size_t workspace_bytes, float* emb_out, void* stream, int32_t nsteps, int32_t exact) {
+  return guarded([&]() -> int {
+    if (!model || !feats || !emb_out || !workspace || B <= 0 || T <= 0) return SPK_E_INVALID;
+    const auto pp = get_pair(model, B, T);
+    if (workspace_bytes < pp->ws_bytes) return SPK_E_WORKSPACE;
+    Plan* p = exact || !pp->x3 ? pp->ex.get() : pp->x3.get();
+    Ctx c{reinterpret_cast<char*>(workspace), feats, emb_out, reinterpret_cast<hipStream_t>(stream)};
+    c.flag = exact ? nullptr : reinterpret_cast<int*>(c.ws + pp->stage_flag);
+    for (int i = 0; i < nsteps && i < (int)p->steps.size(); ++i) {
+      hipError_t e = p->steps[i](c);
+      if (e != hipSuccess) {
+        set_error("step '" + p->names[i] + "': " + hipGetErrorString(e));
+        return SPK_E_HIP;
+      }
+    }
     return SPK_OK;
   });
 }
@@ -638,7 +704,7 @@ int spk_model_range_check(spk_model_t* model, void* stream, int32_t* overflowed)
 int spk_model_plan_size(spk_model_t* model, int32_t B, int32_t T, int32_t* n_steps) {
   return guarded([&]() -> int {
     if (!model || !n_steps || B <= 0 || T <= 0) return SPK_E_INVALID;
-    *n_steps = (int32_t)get_plan(model, B, T)->steps.size();
+    *n_steps = (int32_t)main_plan(get_pair(model, B, T))->steps.size();
     return SPK_OK;
   });
 }
@@ -647,7 +713,8 @@ int spk_model_plan_step(spk_model_t* model, int32_t B, int32_t T, int32_t i, cha
                         char* kernel, int32_t kernel_len, double* flops) {
   return guarded([&]() -> int {
     if (!model || B <= 0 || T <= 0) return SPK_E_INVALID;
-    Plan* p = get_plan(model, B, T);
+    const auto pp = get_pair(model, B, T);
+    Plan* p = main_plan(pp);
     if (i < 0 || i >= (int)p->steps.size()) return SPK_E_INVALID;
     if (name && name_len > 0) { std::strncpy(name, p->names[i].c_str(), name_len - 1); name[name_len - 1] = 0; }
     if (kernel && kernel_len > 0) {
@@ -662,7 +729,8 @@ int spk_model_plan_step(spk_model_t* model, int32_t B, int32_t T, int32_t i, cha
 int spk_model_plan_step_bytes(spk_model_t* model, int32_t B, int32_t T, int32_t i, double* bytes) {
   return guarded([&]() -> int {
     if (!model || !bytes || B <= 0 || T <= 0) return SPK_E_INVALID;
-    Plan* p = get_plan(model, B, T);
+    const auto pp = get_pair(model, B, T);
+    Plan* p = main_plan(pp);
     if (i < 0 || i >= (int)p->steps.size()) return SPK_E_INVALID;
     *bytes = p->bytes[i];
     return SPK_OK;
@@ -673,15 +741,17 @@ int spk_model_forward_timed(spk_model_t* model, const float* feats, int32_t B, i
                             size_t workspace_bytes, float* emb_out, void* stream, float* step_ms, int32_t max_steps) {
   return guarded([&]() -> int {
     if (!model || !feats || !emb_out || !step_ms || B <= 0 || T <= 0) return SPK_E_INVALID;
-    Plan* plan = get_plan(model, B, T);
+    const auto pp = get_pair(model, B, T);
+    Plan* plan = main_plan(pp);
     const int n = (int)plan->steps.size();
     if (max_steps < n) { set_error("spk_model_forward_timed: step_ms too short"); return SPK_E_INVALID; }
-    if (workspace_bytes < plan->ws_bytes) return SPK_E_WORKSPACE;
+    if (workspace_bytes < pp->ws_bytes) return SPK_E_WORKSPACE;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     std::vector<hipEvent_t> ev(n + 1);
     for (auto& e : ev)
       if (int rc = hip_check(hipEventCreate(&e), "hipEventCreate")) return rc;
     Ctx c{reinterpret_cast<char*>(workspace), feats, emb_out, s};
+    c.flag = pp->x3 ? reinterpret_cast<int*>(c.ws + pp->stage_flag) : nullptr;   // no exact re-run here
     int rc = SPK_OK;
     (void)hipEventRecord(ev[0], s);
     for (int i = 0; i < n && rc == SPK_OK; ++i) {

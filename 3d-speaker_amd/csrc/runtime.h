@@ -36,6 +36,7 @@ struct Ctx {
   float* out;
   hipStream_t stream;
   const int* lens = nullptr;   // ragged batches: valid frames per utterance (device int32 [B])
+  int* flag = nullptr;         // this forward's fp16x3 range-guard word (workspace slot; null: exact plan)
   float* resolve(const Buf& b) const {
     switch (b.kind) {
       case Buf::WS: return reinterpret_cast<float*>(ws + b.off);
@@ -57,13 +58,19 @@ struct Plan {
   std::vector<std::string> kernels; // kernel instantiation each step launches
   std::vector<double> flops;        // algorithmic FLOPs of the step (whole batch)
   std::vector<double> bytes;        // algorithmic HBM bytes of the step (each operand once; 0 = not priced)
+  size_t ws_bytes = 0;              // intermediates (the pair adds staging, PlanPair)
+};
+
+// A shape's fp16x3 plan and exact-fp32 plan over one workspace layout: intermediates in
+// [0, max ws), then the staging regions and the range word both plans share.  `graphs`
+// holds the captured forward (fp16x3 steps + gated exact steps) per workspace address.
+struct PlanPair {
+  std::unique_ptr<Plan> x3, ex;     // x3 == null: the handle runs exact only
   size_t ws_bytes = 0;
-  // hipGraph replay: the plan's launches captured once per workspace address, reading the
-  // input / lengths from and writing the output to staging regions of the workspace
-  size_t stage_in = 0, stage_out = 0, stage_len = 0;   // byte offsets in the workspace
+  size_t stage_in = 0, stage_out = 0, stage_len = 0, stage_flag = 0;
   size_t in_bytes = 0, out_bytes = 0, len_bytes = 0;
   std::map<const void*, hipGraphExec_t> graphs;
-  ~Plan();
+  ~PlanPair();
 };
 
 // Logical -> physical channel map of a channels-last tensor (zero-padded slices).
@@ -81,6 +88,7 @@ struct Packed {
   int N = 0, K = 0, Kp = 0;
   size_t ps_off = SIZE_MAX, pt_off = SIZE_MAX;   // optional post-activation affine
   bool has_bias = false;
+  float wmax = 0.f;                               // max |w| of the packed matrix
 };
 
 // One weight tensor's contribution to a packed GEMM.
@@ -105,13 +113,14 @@ struct Model {
   size_t dweights_bytes = 0;
   uint16_t* dsplit = nullptr;                     // fp16 hi plane then lo plane of the whole arena
   std::map<std::string, Packed> packed;
-  // launch plans by (B, T, ragged, exact); at most kMaxPlans are kept (least recently used
-  // evicted: variable-length callers would otherwise grow plans and graphs without bound)
-  std::map<std::tuple<int, int, int, int>, std::unique_ptr<Plan>> plans;
-  std::map<std::tuple<int, int, int, int>, uint64_t> plan_use;
+  // launch plans by (B, T, ragged): the fp16x3 plan and its exact-fp32 twin (the range
+  // guard's gated re-run; the same object when the handle runs exact only), sharing one
+  // workspace layout.  At most kMaxPlans are kept, least recently used evicted; callers hold
+  // a shared_ptr, so an evicted pair lives until its last forward has been enqueued
+  std::map<std::tuple<int, int, int>, std::shared_ptr<PlanPair>> plans;
+  std::map<std::tuple<int, int, int>, uint64_t> plan_use;
   uint64_t plan_clock = 0;
   static constexpr size_t kMaxPlans = 24;
-  int* range_flag = nullptr;                      // device word of the fp16x3 range guard (common.h)
   bool force_exact = false;                       // a packed weight is out of fp16 range: exact path only
   bool fp16 = false;                              // SPK_PRECISION_FP16: single-product fp16 GEMMs
   float gemm_wmax = 0.f;                          // max |w| over the packed GEMM weights

@@ -28,7 +28,8 @@ __device__ __forceinline__ int valid_frames(const int* vlen, int b, int T) {
 }
 
 __global__ void time_mean_kernel(const float* __restrict__ x, int B, int T, int C, int ld, float* __restrict__ out,
-                                 int ldo, const int* __restrict__ vlen) {
+                                 int ldo, const int* __restrict__ vlen, const int* __restrict__ run_if) {
+  SPK_GATE(run_if);
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
        e += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(e % C), b = (int)(e / C);
@@ -41,7 +42,8 @@ __global__ void time_mean_kernel(const float* __restrict__ x, int B, int T, int 
 }
 
 __global__ void asp_stats_kernel(const float* __restrict__ x, int B, int T, int C, int ld, float eps,
-                                 float* __restrict__ out, const int* __restrict__ vlen) {
+                                 float* __restrict__ out, const int* __restrict__ vlen, const int* __restrict__ run_if) {
+  SPK_GATE(run_if);
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
        e += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(e % C), b = (int)(e / C);
@@ -61,7 +63,8 @@ __global__ void asp_stats_kernel(const float* __restrict__ x, int B, int T, int 
 }
 
 __global__ void attn_pool_kernel(const float* __restrict__ logit, int ldl, const float* __restrict__ x, int ldx, int B,
-                                 int T, int C, float eps, float* __restrict__ out, const int* __restrict__ vlen) {
+                                 int T, int C, float eps, float* __restrict__ out, const int* __restrict__ vlen, const int* __restrict__ run_if) {
+  SPK_GATE(run_if);
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
        e += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(e % C), b = (int)(e / C);
@@ -93,7 +96,8 @@ __global__ void attn_pool_kernel(const float* __restrict__ logit, int ldl, const
 
 __global__ void se_apply_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ gate, int ldg,
                                 const float* __restrict__ res, int ldr, float* __restrict__ out, int ldo, int B, int T,
-                                int C) {
+                                int C, const int* __restrict__ run_if) {
+  SPK_GATE(run_if);
   const int C4 = C / 4;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * T * C4;
        e += (long long)gridDim.x * blockDim.x) {
@@ -112,7 +116,8 @@ __global__ void se_apply_kernel(const float* __restrict__ x, int ldx, const floa
 // ctx[b, s, c] = mean_T(x)[b, c] + mean over frames [100 s, min(100 s + 100, T)) of x[b, :, c]
 // (ragged batches: utterance b has vlen[b] valid frames; segments past them are written as 0)
 __global__ void cam_context_kernel(const float* __restrict__ x, int B, int T, int C, int ld, int seg, int nseg,
-                                   float* __restrict__ out, int ldo, const int* __restrict__ vlen) {
+                                   float* __restrict__ out, int ldo, const int* __restrict__ vlen, const int* __restrict__ run_if) {
+  SPK_GATE(run_if);
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
        e += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(e % C), b = (int)(e / C);
@@ -141,7 +146,8 @@ __global__ void cam_context_kernel(const float* __restrict__ x, int B, int T, in
 //    contexts, and both layers with the weights staged transposed in LDS.
 __global__ void __launch_bounds__(256)
 cam_segsum_kernel(const float* __restrict__ x, int T, int C, int ld, int seg, int nseg, float* __restrict__ segsum,
-                  const int* __restrict__ vlen) {
+                  const int* __restrict__ vlen, const int* __restrict__ run_if) {
+  SPK_GATE(run_if);
   __shared__ f32x4 part[256];
   const int sg = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int Tb = valid_frames(vlen, b, T);
@@ -174,7 +180,8 @@ __global__ void __launch_bounds__(1024)
 cam_gate_kernel(const float* __restrict__ segsum, int T, int C, int seg, int nseg, const float* __restrict__ w1,
                 int k1p, const float* __restrict__ b1, int red, const float* __restrict__ w2, int k2p,
                 const float* __restrict__ b2, int growth, float* __restrict__ gate, int ldg,
-                const int* __restrict__ vlen) {
+                const int* __restrict__ vlen, const int* __restrict__ run_if) {
+  SPK_GATE(run_if);
   extern __shared__ float sm[];
   float* w1t = sm;                          // [C][red + 1]  (transposed, padded: conflict-free)
   float* w2t = w1t + C * (red + 1);         // [red][growth + 1]
@@ -244,7 +251,8 @@ cam_gate_kernel(const float* __restrict__ segsum, int T, int C, int seg, int nse
 }
 
 __global__ void stats_pool_kernel(const float* __restrict__ x, int B, int T, int C, int ld, float* __restrict__ out,
-                                  const int* __restrict__ vlen) {
+                                  const int* __restrict__ vlen, const int* __restrict__ run_if) {
+  SPK_GATE(run_if);
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * C;
        e += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(e % C), b = (int)(e / C);
@@ -263,7 +271,8 @@ __global__ void stats_pool_kernel(const float* __restrict__ x, int B, int T, int
 }
 
 // out[b] = (in[b] + 2 pad - k) / stride + 1: valid output frames of a strided conv
-__global__ void derive_len_kernel(const int* __restrict__ in, int* __restrict__ out, int B, int pad, int k, int stride) {
+__global__ void derive_len_kernel(const int* __restrict__ in, int* __restrict__ out, int B, int pad, int k, int stride, const int* __restrict__ run_if) {
+  SPK_GATE(run_if);
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b < B) out[b] = (in[b] + 2 * pad - k) / stride + 1;
 }
@@ -273,21 +282,21 @@ __global__ void derive_len_kernel(const int* __restrict__ in, int* __restrict__ 
 hipError_t launch_time_mean(const float* x, int B, int T, int C, int ld, float* out, int ldo, hipStream_t s,
                             const int* vlen) {
   hipLaunchKernelGGL(time_mean_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, out, ldo,
-                     vlen);
+                     vlen, launch_gate());
   return hipGetLastError();
 }
 
 hipError_t launch_asp_stats(const float* x, int B, int T, int C, int ld, float eps, float* out, hipStream_t s,
                             const int* vlen) {
   hipLaunchKernelGGL(asp_stats_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, eps, out,
-                     vlen);
+                     vlen, launch_gate());
   return hipGetLastError();
 }
 
 hipError_t launch_attn_pool(const float* logit, int ldl, const float* x, int ldx, int B, int T, int C, float eps,
                             float* out, hipStream_t s, const int* vlen) {
   hipLaunchKernelGGL(attn_pool_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, logit, ldl, x, ldx, B, T, C,
-                     eps, out, vlen);
+                     eps, out, vlen, launch_gate());
   return hipGetLastError();
 }
 
@@ -295,14 +304,14 @@ hipError_t launch_se_apply(const float* x, int ldx, const float* gate, int ldg, 
                            int ldo, int B, int T, int C, hipStream_t s) {
   if (C % 4 || ldx % 4 || ldg % 4 || ldr % 4 || ldo % 4) return hipErrorInvalidValue;
   hipLaunchKernelGGL(se_apply_kernel, dim3(grid_for((long long)B * T * C / 4)), dim3(256), 0, s, x, ldx, gate, ldg,
-                     res, ldr, out, ldo, B, T, C);
+                     res, ldr, out, ldo, B, T, C, launch_gate());
   return hipGetLastError();
 }
 
 hipError_t launch_cam_context(const float* x, int B, int T, int C, int ld, int seg, int nseg, float* out, int ldo,
                               hipStream_t s, const int* vlen) {
   hipLaunchKernelGGL(cam_context_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, seg, nseg,
-                     out, ldo, vlen);
+                     out, ldo, vlen, launch_gate());
   return hipGetLastError();
 }
 
@@ -311,23 +320,23 @@ hipError_t launch_cam_gate(const float* x, int B, int T, int C, int ld, int seg,
                           int ldg, float* segsum, hipStream_t s, const int* vlen) {
   if (C % 4 || C / 4 > 256 || ld % 4 || red <= 0 || red > 1024 || growth <= 0 || growth > 1024 || B <= 0 || nseg <= 0)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(cam_segsum_kernel, dim3(nseg, B), dim3(256), 0, s, x, T, C, ld, seg, nseg, segsum, vlen);
+  hipLaunchKernelGGL(cam_segsum_kernel, dim3(nseg, B), dim3(256), 0, s, x, T, C, ld, seg, nseg, segsum, vlen, launch_gate());
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   const size_t lds = sizeof(float) * ((size_t)C * (red + 1) + (size_t)red * (growth + 1) + C +
                                       CAM_SEGS * (C + red + 1024));
   if (lds > 64 * 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(cam_gate_kernel, dim3(B), dim3(1024), lds, s, segsum, T, C, seg, nseg, w1, k1p, b1, red, w2, k2p,
-                     b2, growth, gate, ldg, vlen);
+                     b2, growth, gate, ldg, vlen, launch_gate());
   return hipGetLastError();
 }
 
 hipError_t launch_stats_pool(const float* x, int B, int T, int C, int ld, float* out, hipStream_t s, const int* vlen) {
-  hipLaunchKernelGGL(stats_pool_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, out, vlen);
+  hipLaunchKernelGGL(stats_pool_kernel, dim3(grid_for((long long)B * C)), dim3(256), 0, s, x, B, T, C, ld, out, vlen, launch_gate());
   return hipGetLastError();
 }
 
 hipError_t launch_derive_len(const int* in, int* out, int B, int pad, int k, int stride, hipStream_t s) {
-  hipLaunchKernelGGL(derive_len_kernel, dim3((B + 255) / 256), dim3(256), 0, s, in, out, B, pad, k, stride);
+  hipLaunchKernelGGL(derive_len_kernel, dim3((B + 255) / 256), dim3(256), 0, s, in, out, B, pad, k, stride, launch_gate());
   return hipGetLastError();
 }
 

@@ -70,7 +70,8 @@ SYMBOLS = {
     'spk_model_forward_lengths': (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_size_t, _P,
                                                  _P]),
     'spk_model_flops': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_double)]),
-    'spk_model_range_check': (ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_int32)]),
+    'spk_model_range_check': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P,
+                                             ctypes.POINTER(ctypes.c_int32)]),
     'spk_model_forward_exact': (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_size_t, _P,
                                                _P]),
     'spk_model_plan_size': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
@@ -244,7 +245,7 @@ class NativeModel:
         self.handle = handle
         self._ws: Optional[torch.Tensor] = None          # workspace of the last forward
         self._ws_by_stream = {}                           # stream handle -> workspace
-        self.last_forward_exact = False
+        self._last = None                                 # (B, T, ragged, workspace, stream) of the last forward
 
     def __del__(self):
         h = getattr(self, 'handle', None)
@@ -354,19 +355,22 @@ class NativeModel:
                                                        self._ws.data_ptr(), self._ws.numel(), out.data_ptr(),
                                                        _stream(self.device)),
                        'spk_model_forward_lengths')
-            # fp16x3 range guard (include/spk_hip.h): an activation reached fp16's range ->
-            # the same forward again on the exact-fp32 kernels
-            flag = ctypes.c_int32(0)
-            _check(lib().spk_model_range_check(self.handle, _stream(self.device), ctypes.byref(flag)),
-                   'spk_model_range_check')
-            self.last_forward_exact = bool(flag.value)
-            if flag.value:
-                _check(lib().spk_model_forward_exact(self.handle, feats.data_ptr(), B, T,
-                                                     None if lengths is None else lengths.data_ptr(),
-                                                     self._ws.data_ptr(), self._ws.numel(), out.data_ptr(),
-                                                     _stream(self.device)),
-                       'spk_model_forward_exact')
+            # the fp16x3 range guard resolves on the device (include/spk_hip.h): no host sync
+            self._last = (B, T, int(lengths is not None), self._ws, _stream(self.device))
         return out
+
+    @property
+    def last_forward_exact(self) -> bool:
+        """Whether the last forward was recomputed on the exact-fp32 kernels because an
+        activation reached fp16's range (synchronises that forward's stream; diagnostics)."""
+        if self._last is None:
+            return False
+        B, T, ragged, ws, stream = self._last
+        flag = ctypes.c_int32(0)
+        with torch.cuda.device(self.device):
+            _check(lib().spk_model_range_check(self.handle, B, T, ragged, ws.data_ptr(), stream, ctypes.byref(flag)),
+                   'spk_model_range_check')
+        return bool(flag.value)
 
 
 class HipModuleMixin:

@@ -20,6 +20,31 @@ import time
 import numpy as np
 import torch
 
+# The GPU Fbank implements exactly the runtime's shipped options (assets/fbank_config.json):
+# 16 kHz, 25 ms windows every 10 ms, no dither, power spectrum.  Any other value would be
+# computed with these settings instead, so it is refused.
+_FIXED = {('FrameExtractionOptions', 'sample_freq'): 16000.0,
+          ('FrameExtractionOptions', 'frame_length_ms'): 25.0,
+          ('FrameExtractionOptions', 'frame_shift_ms'): 10.0,
+          ('FrameExtractionOptions', 'dither'): 0.0,
+          ('use_power',): True}
+
+
+def check_fbank_config(cfg: dict) -> int:
+    """Validate a runtime Fbank JSON against what the kernel computes; returns num_bins."""
+    for path, want in _FIXED.items():
+        node = cfg
+        for k in path:
+            node = node.get(k, want) if isinstance(node, dict) else want
+        ok = (bool(node) == want) if isinstance(want, bool) else float(node) == want
+        if not ok:
+            raise ValueError(f'fbank config {".".join(path)} = {node!r}: the MI355X Fbank kernel implements '
+                             f'{want!r} only')
+    n_mels = int(cfg.get('MelBanksOptions', {}).get('num_bins', 80))
+    if not 3 < n_mels <= 128:
+        raise ValueError(f'fbank config MelBanksOptions.num_bins = {n_mels}: supported range is 4..128')
+    return n_mels
+
 
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
@@ -34,8 +59,8 @@ def main(argv=None):
     from speakerlab.utils.builder import dynamic_import
     with open(config_file) as f:
         cfg = json.load(f)
-    fs = int(cfg.get('FrameExtractionOptions', {}).get('sample_freq', 16000))
-    n_mels = int(cfg.get('MelBanksOptions', {}).get('num_bins', 80))
+    n_mels = check_fbank_config(cfg)
+    fs = 16000
     model_id, _, ckpt = model_arg.partition('=')
     if model_id not in isb.supports:
         raise ValueError(f'{model_id} is not in the model registry (speakerlab/bin/infer_sv_batch.py)')

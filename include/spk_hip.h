@@ -6,9 +6,10 @@
  * Every entry point returns 0 on success or a negative SPK_E_* code; the message of the
  * last failure on the calling thread is available from spk_last_error().  No C++
  * exception crosses this boundary.  Handles are immutable after creation, so one handle
- * may be used from several streams concurrently; forward() allocates nothing (the caller
- * provides a workspace sized by spk_model_workspace_bytes()), so it can be captured into
- * a hipGraph.
+ * may be used from several streams concurrently, each forward with its own workspace (all
+ * per-forward state, the fp16x3 range word included, lives in the workspace); forward()
+ * allocates nothing (the caller provides a workspace sized by spk_model_workspace_bytes())
+ * and never synchronises the host, so it can be captured into a hipGraph.
  *
  * Which reference interface each entry point replaces (paths relative to the reference
  * repo nanless/3D-Speaker):
@@ -135,15 +136,22 @@ int spk_model_workspace_bytes_lengths(spk_model_t* model, int32_t B, int32_t T, 
 int spk_model_forward_lengths(spk_model_t* model, const float* feats, int32_t B, int32_t T, const int32_t* lengths,
                               void* workspace, size_t workspace_bytes, float* emb_out, void* stream);
 
-/* fp16x3 range guard.  The default kernels represent every GEMM operand as two fp16 values
- * (fp32-accurate, csrc/conv_gemm.hip); a value at or past fp16's range (65504) would
- * saturate.  Every producer of an unbounded activation (and the input check) sets a device
- * flag of the handle when a value reaches 2^15; spk_model_range_check() synchronises the
- * stream, reports and clears it, and spk_model_forward_exact() (same arguments as
- * spk_model_forward_lengths, lengths may be NULL) runs the same forward on exact-fp32 MFMA
- * kernels only.  A handle whose packed weights leave fp16's range always runs exact.  The
- * workspace queries return the larger of the two plans' needs. */
-int spk_model_range_check(spk_model_t* model, void* stream, int32_t* overflowed);
+/* fp16x3 range guard, resolved on the device.  The default kernels represent every GEMM
+ * operand as two fp16 values (fp32-accurate, csrc/conv_gemm.hip); a value at or past fp16's
+ * range (65504) would saturate.  Every producer of an unbounded activation (and the input
+ * check) sets a range word in the caller's workspace -- one per forward, zeroed when the
+ * forward starts -- when a value reaches 2^14; the forward then re-runs itself on exact-fp32
+ * MFMA kernels, launched behind it on the same stream and gated on that word, and the exact
+ * embeddings replace the split ones.  spk_model_forward* therefore only enqueue (no host
+ * synchronisation), and concurrent forwards on different streams with different workspaces
+ * never see each other's word.  spk_model_range_check() reports (synchronising `stream`)
+ * whether the last forward of shape (B, T, ragged) that used `workspace` took the exact
+ * re-run (diagnostics).  spk_model_forward_exact() (same arguments as
+ * spk_model_forward_lengths, lengths may be NULL) runs the exact plan only.  A handle whose
+ * packed weights leave fp16's range always runs exact.  The workspace queries cover both
+ * plans. */
+int spk_model_range_check(spk_model_t* model, int32_t B, int32_t T, int32_t ragged, const void* workspace,
+                          void* stream, int32_t* overflowed);
 int spk_model_forward_exact(spk_model_t* model, const float* feats, int32_t B, int32_t T, const int32_t* lengths,
                             void* workspace, size_t workspace_bytes, float* emb_out, void* stream);
 

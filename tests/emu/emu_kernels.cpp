@@ -23,6 +23,10 @@
 
 namespace spk {
 
+// launches of the gated exact plan do nothing unless the forward's range word is set
+// (common.h SPK_GATE; the gate pointer is host memory here)
+#define EMU_GATE() do { if (const int* g_ = spk::launch_gate()) { if (*g_ == 0) return hipSuccess; } } while (0)
+
 static float act_f(float v, int act) {
   switch (act) {
     case ACT_RELU: return v > 0.f ? v : 0.f;
@@ -53,6 +57,7 @@ static float epilogue(const ConvDesc& d, int m, int n, float v) {
 }
 
 hipError_t launch_conv(const ConvDesc& d, hipStream_t) {
+  EMU_GATE();
   if (d.s0.cin % 4 || d.s0.ld % 4 || d.Kp % 16 || (d.osplit ? (d.osplit % 4 || d.ldo < d.osplit) : d.ldo < d.N) || d.K > d.Kp) return hipErrorInvalidValue;
   const int M = d.nimg * d.Ho * d.Wo;
   const int K0 = d.s0.kh * d.s0.kw * d.s0.cin;
@@ -104,6 +109,7 @@ std::string conv_kernel_name(const ConvDesc&) { return "emu_conv"; }
 bool aff_x3_supported(int cp, int nmid) { return (nmid == 32 || nmid == 64) && cp % 8 == 0 && cp >= 8 && cp <= 208; }
 std::string aff_x3_kernel_name(int nmid) { return "emu_aff<" + std::to_string(nmid / 32) + ">"; }
 hipError_t launch_aff_x3(const AffDesc& a, hipStream_t) {
+  EMU_GATE();
   if (!aff_x3_supported(a.cp, a.nmid) || a.kp1 < 2 * a.cp || a.kp2 < a.nmid) return hipErrorInvalidValue;
   std::vector<double> h(a.nmid);
   for (int m = 0; m < a.M; ++m) {
@@ -128,19 +134,27 @@ hipError_t launch_aff_x3(const AffDesc& a, hipStream_t) {
 }
 
 // the emulated GEMM reads the fp32 weights; the split planes are not needed on the host
-hipError_t launch_split_f16(const float*, uint16_t*, uint16_t*, size_t, hipStream_t) { return hipSuccess; }
+hipError_t launch_split_f16(const float*, uint16_t*, uint16_t*, size_t, hipStream_t) {
+  EMU_GATE(); return hipSuccess; }
 
 static void emu_range_note(int* flag, float v) {   // common.h range guard
   if (flag && std::fabs(v) >= kRangeLimit) *flag |= 1;
 }
 
+hipError_t launch_word_reset(int* w, hipStream_t) {
+  *w = 0;
+  return hipSuccess;
+}
+
 hipError_t launch_range_check(const float* x, size_t n, int* flag, hipStream_t) {
+  EMU_GATE();
   for (size_t i = 0; i < n; ++i) emu_range_note(flag, x[i]);
   return hipSuccess;
 }
 
 hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const float* w, const float* bias, int cout,
                                int act, int wstride, float* out, int ldo, hipStream_t, const int* vlen, int* range_flag) {
+  EMU_GATE();
   for (int b = 0; b < B; ++b) {
     const int Tb = vlen ? vlen[b] : T;
     for (int f = 0; f < F; ++f)
@@ -163,6 +177,7 @@ hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const fl
 
 hipError_t launch_tstp(const float* x, int B, int H, int W, int C, int ld, float eps, int unbiased, float* out,
                        hipStream_t, int parts) {
+  EMU_GATE();
   const int np = (parts & 1) + ((parts >> 1) & 1);
   for (int b = 0; b < B; ++b)
     for (int h = 0; h < H; ++h)
@@ -183,6 +198,7 @@ hipError_t launch_tstp(const float* x, int B, int H, int W, int C, int ld, float
 
 hipError_t launch_fbank(const float*, const int64_t*, int, float*, const int64_t*, int, int, const FbankTables*, int,
                         hipStream_t, int) {
+  EMU_GATE();
   return hipErrorNotSupported;
 }
 
@@ -202,6 +218,7 @@ bool res2_block_supported(const Res2Desc& d) {
 }
 std::string res2_block_kernel_name(const Res2Desc& d) { return "emu_res2_block<" + std::to_string(d.C) + ">"; }
 hipError_t launch_res2_block(const Res2Desc& d, hipStream_t) {
+  EMU_GATE();
   if (!res2_block_supported(d) || d.x == d.out) return hipErrorInvalidValue;
   const int H = d.H, W = d.W, C = d.C, CO = d.Cout ? d.Cout : d.C, K3 = d.proj ? 64 + C : 64;
   auto ht = [](double v) { return std::min(std::max(v, 0.0), 20.0); };
@@ -253,15 +270,18 @@ hipError_t launch_res2_block(const Res2Desc& d, hipStream_t) {
 size_t cosine_topk_workspace(long long, long long) { return 0; }
 hipError_t launch_cosine_topk(const float*, long long, const float*, long long, int, int, long long, int, float, void*,
                               size_t, float*, long long*, long long*, hipStream_t) {
+  EMU_GATE();
   return hipErrorNotSupported;
 }
 hipError_t launch_cosine_trials(const float*, const float*, int, const long long*, const long long*, long long, float*,
                                 hipStream_t) {
+  EMU_GATE();
   return hipErrorNotSupported;
 }
 
 hipError_t launch_cosine_affinity(const float* A, long long Na, const float* B, long long Nb, int E, float* out,
                                   long long ldo, hipStream_t) {
+  EMU_GATE();
   for (long long i = 0; i < Na; ++i)
     for (long long j = 0; j < Nb; ++j) {
       double d = 0, na = 0, nb = 0;
@@ -323,6 +343,7 @@ namespace spk {
 static int vframes(const int* vlen, int b, int T) { return vlen ? std::min(std::max(vlen[b], 1), T) : T; }
 hipError_t launch_time_mean(const float* x, int B, int T, int C, int ld, float* out, int ldo, hipStream_t,
                             const int* vlen) {
+  EMU_GATE();
   for (int b = 0; b < B; ++b)
     for (int c = 0; c < C; ++c) {
       const int Tb = vframes(vlen, b, T);
@@ -334,6 +355,7 @@ hipError_t launch_time_mean(const float* x, int B, int T, int C, int ld, float* 
 }
 hipError_t launch_asp_stats(const float* x, int B, int T, int C, int ld, float eps, float* out, hipStream_t,
                             const int* vlen) {
+  EMU_GATE();
   for (int b = 0; b < B; ++b)
     for (int c = 0; c < C; ++c) {
       const int Tb = vframes(vlen, b, T);
@@ -348,6 +370,7 @@ hipError_t launch_asp_stats(const float* x, int B, int T, int C, int ld, float e
 }
 hipError_t launch_attn_pool(const float* l, int ldl, const float* x, int ldx, int B, int T, int C, float eps,
                             float* out, hipStream_t, const int* vlen) {
+  EMU_GATE();
   std::vector<double> p(T);
   for (int b = 0; b < B; ++b)
     for (int c = 0; c < C; ++c) {
@@ -364,6 +387,7 @@ hipError_t launch_attn_pool(const float* l, int ldl, const float* x, int ldx, in
 }
 hipError_t launch_se_apply(const float* x, int ldx, const float* g, int ldg, const float* r, int ldr, float* out,
                            int ldo, int B, int T, int C, hipStream_t) {
+  EMU_GATE();
   for (int b = 0; b < B; ++b)
     for (int t = 0; t < T; ++t)
       for (int c = 0; c < C; ++c) {
@@ -375,6 +399,7 @@ hipError_t launch_se_apply(const float* x, int ldx, const float* g, int ldg, con
 hipError_t launch_cam_gate(const float* x, int B, int T, int C, int ld, int seg, int nseg, const float* w1, int k1p,
                           const float* b1, int red, const float* w2, int k2p, const float* b2, int growth, float* gate,
                           int ldg, float*, hipStream_t, const int* vlen) {
+  EMU_GATE();
   std::vector<double> ctx(C), h(red);
   for (int b = 0; b < B; ++b) {
     const int Tb = vlen ? std::min(std::max(vlen[b], 1), T) : T;
@@ -402,6 +427,7 @@ hipError_t launch_cam_gate(const float* x, int B, int T, int C, int ld, int seg,
 }
 hipError_t launch_cam_context(const float* x, int B, int T, int C, int ld, int seg, int nseg, float* out, int ldo,
                               hipStream_t, const int* vlen) {
+  EMU_GATE();
   for (int b = 0; b < B; ++b) {
     const int Tb = vlen ? vlen[b] : T;
     for (int c = 0; c < C; ++c) {
@@ -418,6 +444,7 @@ hipError_t launch_cam_context(const float* x, int B, int T, int C, int ld, int s
   return hipSuccess;
 }
 hipError_t launch_stats_pool(const float* x, int B, int T, int C, int ld, float* out, hipStream_t, const int* vlen) {
+  EMU_GATE();
   for (int b = 0; b < B; ++b) {
     const int Tb = vlen ? vlen[b] : T;
     for (int c = 0; c < C; ++c) {
@@ -432,6 +459,7 @@ hipError_t launch_stats_pool(const float* x, int B, int T, int C, int ld, float*
   return hipSuccess;
 }
 hipError_t launch_derive_len(const int* in, int* out, int B, int pad, int k, int stride, hipStream_t) {
+  EMU_GATE();
   for (int b = 0; b < B; ++b) out[b] = (in[b] + 2 * pad - k) / stride + 1;
   return hipSuccess;
 }

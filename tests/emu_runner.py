@@ -38,7 +38,8 @@ class EmuModel:
         cfg = module._hip_config()
         c = _hip.spk_model_config_t()
         c.arch = module._hip_arch
-        for k in ('feat_dim', 'embed_dim', 'm_channels', 'base_width', 'scale', 'expansion', 'two_emb_layer'):
+        for k in ('feat_dim', 'embed_dim', 'm_channels', 'base_width', 'scale', 'expansion', 'two_emb_layer',
+                  'pooling'):
             setattr(c, k, int(cfg.get(k, 0)))
         for k in ('channels', 'kernel_sizes', 'dilations'):
             vals = list(cfg.get(k, []))[:5]
@@ -59,19 +60,28 @@ class EmuModel:
         self.handle = ctypes.c_void_p()
         _check(lib().spk_model_create(ctypes.byref(c), ws, len(sd), ctypes.byref(self.handle)), 'create')
 
-    def __call__(self, feats, lengths=None):
+    def __call__(self, feats, lengths=None, ws=None):
         feats = feats.float().contiguous()
         B, T, _ = feats.shape
         n = ctypes.c_size_t()
         _check(lib().spk_model_workspace_bytes_lengths(self.handle, B, T, int(lengths is not None), ctypes.byref(n)),
                'workspace')
-        ws = torch.zeros(max(n.value, 256), dtype=torch.uint8)
+        if ws is None:
+            ws = torch.zeros(max(n.value, 256), dtype=torch.uint8)
+        self.last = (B, T, int(lengths is not None), ws)
         out = torch.empty(B, self.embed_dim)
         lens = None if lengths is None else torch.as_tensor(lengths, dtype=torch.int32).contiguous()
         _check(lib().spk_model_forward_lengths(self.handle, feats.data_ptr(), B, T,
                                                None if lens is None else lens.data_ptr(), ws.data_ptr(), ws.numel(),
                                                out.data_ptr(), None), 'forward')
         return out
+
+    def range_word(self, last=None):
+        """spk_model_range_check of the last forward (or of `last` = (B, T, ragged, ws))."""
+        B, T, rg, ws = last or self.last
+        v = ctypes.c_int32(-1)
+        _check(lib().spk_model_range_check(self.handle, B, T, rg, ws.data_ptr(), None, ctypes.byref(v)), 'range_check')
+        return v.value
 
     def plan(self, B, T):
         n = ctypes.c_int32()

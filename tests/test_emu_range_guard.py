@@ -1,7 +1,10 @@
 """fp16x3 range guard plumbing on the host emulation (tests/emu): a model whose activations
-reach 2^15 raises the handle's flag (spk_model_range_check reports and clears it), the exact
-plan (spk_model_forward_exact) reproduces the oracle, and weights past fp16's range force the
-exact path at creation.  The GPU test (tests/test_gpu_range_guard.py) checks the kernels."""
+reach the range limit raises the forward's range word (a workspace slot), the gated exact
+plan captured behind the split one then recomputes the batch (the forward's output
+reproduces the oracle), the word belongs to its workspace (two interleaved forwards with two
+workspaces do not see each other's), spk_model_forward_exact runs the exact plan alone, and
+weights past fp16's range force the exact path at creation.  The GPU test
+(tests/test_gpu_range_guard.py) checks the kernels."""
 import ctypes
 
 import numpy as np
@@ -20,9 +23,7 @@ def _scaled(arch, key, factor):
 
 
 def _flag(em):
-    v = ctypes.c_int32(-1)
-    _check(lib().spk_model_range_check(em.handle, None, ctypes.byref(v)), 'range_check')
-    return v.value
+    return em.range_word()
 
 
 def _forward_exact(em, feats):
@@ -48,14 +49,37 @@ def test_large_activations_flag_and_exact_path():
     m = _scaled('ecapa', 'blocks.0.norm.norm.weight', 1e5)     # post-ReLU BN: activations ~1e5
     feats = torch.from_numpy(g['feats2'][:1])
     em = EmuModel(m)
-    em(feats)
+    guarded = em(feats).numpy()
     assert _flag(em) == 1
-    assert _flag(em) == 0                                       # cleared by the check
-    out = _forward_exact(em, feats).numpy()
+    assert _flag(em) == 1                                       # reading does not clear it
     ref = models_ref.forward('ecapa', {k: v.double() if v.is_floating_point() else v
                                        for k, v in m.state_dict().items()}, feats.double()).numpy()
+    assert helpers.rel_err(guarded, ref).max() < 1e-4           # the gated exact re-run ran
+    out = _forward_exact(em, feats).numpy()
     assert helpers.rel_err(out, ref).max() < 1e-4
-    assert _flag(em) == 0                                       # the exact plan does not flag
+
+
+def test_range_word_is_per_workspace():
+    """Two forwards interleaved with their own workspaces: only the overflowing one is
+    re-run, and a later clean forward on a workspace clears that workspace's word."""
+    g = helpers.golden('campplus')
+    m = helpers.loaded_module('campplus')
+    em = EmuModel(m)
+    clean = torch.from_numpy(g['feats2'][:1]).clone()
+    hot = clean.clone()
+    hot[0, 3, 5] = 40000.0
+    B, T, _ = clean.shape
+    n = ctypes.c_size_t()
+    _check(lib().spk_model_workspace_bytes(em.handle, B, T, ctypes.byref(n)), 'workspace')
+    wa, wb = (torch.zeros(n.value, dtype=torch.uint8) for _ in range(2))
+    sd = {k: v.double() if v.is_floating_point() else v for k, v in m.state_dict().items()}
+    oa = em(hot, ws=wa).numpy()
+    ob = em(clean, ws=wb).numpy()
+    assert em.range_word((B, T, 0, wa)) == 1 and em.range_word((B, T, 0, wb)) == 0
+    assert helpers.rel_err(oa, models_ref.forward('campplus', sd, hot.double()).numpy()).max() < 1e-4
+    assert helpers.rel_err(ob, models_ref.forward('campplus', sd, clean.double()).numpy()).max() < 1e-4
+    em(clean, ws=wa)
+    assert em.range_word((B, T, 0, wa)) == 0
 
 
 def test_large_input_flags():

@@ -1,8 +1,11 @@
 """fp16x3 range guard on the GPU (include/spk_hip.h): models whose activations leave the
 range the split-precision GEMMs represent (ECAPA / CAM++ have unbounded ReLU -> BN outputs,
 ECAPA_TDNN.py:127-151, layers.py:40-67) still match the fp64 reference forward within the
-north-star 1e-4, because the flagged forward is re-run on the exact-fp32 kernels; the fp16x3
-result alone would not (the saturation the guard exists for)."""
+north-star 1e-4, because the flagged forward is re-run on the exact-fp32 kernels (captured
+behind it and gated on the forward's range word, no host round trip); the fp16x3 result
+alone would not (the saturation the guard exists for).  The word lives in the forward's
+workspace: two forwards enqueued on two streams with no synchronisation between them, one
+of them overflowing, re-run only that one."""
 import ctypes
 
 import numpy as np
@@ -46,8 +49,15 @@ def test_out_of_range_activations_take_exact_path(arch, key, factor):
     _hip._check(_hip.lib().spk_model_forward(h.handle, x.data_ptr(), B, T, ws.data_ptr(), ws.numel(),
                                              raw.data_ptr(), _hip._stream(dev)), 'forward')
     flag = ctypes.c_int32(0)
-    _hip._check(_hip.lib().spk_model_range_check(h.handle, _hip._stream(dev), ctypes.byref(flag)), 'check')
+    _hip._check(_hip.lib().spk_model_range_check(h.handle, B, T, 0, ws.data_ptr(), _hip._stream(dev),
+                                                 ctypes.byref(flag)), 'check')
     assert flag.value == 1
+    # the guarded forward already replaced the split result; the split plan alone (timed
+    # forward: no exact re-run) saturates, far off the reference
+    ms = (ctypes.c_float * 512)()
+    _hip._check(_hip.lib().spk_model_forward_timed(h.handle, x.data_ptr(), B, T, ws.data_ptr(), ws.numel(),
+                                                   raw.data_ptr(), _hip._stream(dev), ms, 512), 'timed')
+    torch.cuda.synchronize()
     assert helpers.rel_err(raw.cpu().numpy(), ref).max() > 1e-3
 
 
@@ -58,3 +68,40 @@ def test_in_range_model_stays_on_split_path():
     with torch.no_grad():
         m(torch.from_numpy(g['feats2'][:2]).to(dev))
     assert not m._hip_handle(dev).last_forward_exact
+
+
+def test_two_streams_only_the_overflowing_forward_reruns():
+    g = helpers.golden('campplus')
+    m = helpers.loaded_module('campplus')
+    sd = {k: v.double() if v.is_floating_point() else v for k, v in m.state_dict().items()}
+    clean = torch.from_numpy(g['feats2'][:4]).clone()
+    hot = clean.clone()
+    hot[1, 7, 11] = 40000.0                 # model input past the range limit: row 1 only
+    ref_hot = models_ref.forward('campplus', sd, hot.double()).numpy()
+    ref_clean = models_ref.forward('campplus', sd, clean.double()).numpy()
+    dev = torch.device('cuda', 0)
+    m = m.to(dev)
+    h = m._hip_handle(dev)
+    B, T, _ = clean.shape
+    xa, xb = hot.to(dev).contiguous(), clean.to(dev).contiguous()
+    need = h.workspace_bytes(B, T)
+    sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    wa = torch.empty(need, dtype=torch.uint8, device=dev)
+    wb = torch.empty(need, dtype=torch.uint8, device=dev)
+    oa = torch.empty(B, h.embed_dim, device=dev)
+    ob = torch.empty(B, h.embed_dim, device=dev)
+    torch.cuda.synchronize()
+    for _ in range(3):                      # both forwards in flight together, no sync between
+        _hip._check(_hip.lib().spk_model_forward(h.handle, xa.data_ptr(), B, T, wa.data_ptr(), need,
+                                                 oa.data_ptr(), sa.cuda_stream), 'forward a')
+        _hip._check(_hip.lib().spk_model_forward(h.handle, xb.data_ptr(), B, T, wb.data_ptr(), need,
+                                                 ob.data_ptr(), sb.cuda_stream), 'forward b')
+    torch.cuda.synchronize()
+    fa, fb = ctypes.c_int32(-1), ctypes.c_int32(-1)
+    _hip._check(_hip.lib().spk_model_range_check(h.handle, B, T, 0, wa.data_ptr(), sa.cuda_stream, ctypes.byref(fa)),
+                'check a')
+    _hip._check(_hip.lib().spk_model_range_check(h.handle, B, T, 0, wb.data_ptr(), sb.cuda_stream, ctypes.byref(fb)),
+                'check b')
+    assert fa.value == 1 and fb.value == 0
+    assert helpers.rel_err(oa.cpu().numpy(), ref_hot).max() < 1e-4
+    assert helpers.rel_err(ob.cpu().numpy(), ref_clean).max() < 1e-4

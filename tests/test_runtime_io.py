@@ -91,3 +91,20 @@ def test_embedding_file_roundtrip(tmp_path):
     runtime_io.write_runtime_embedding(str(tmp_path / 'e.embedding'), v)
     back = runtime_io.read_runtime_embedding(str(tmp_path / 'e.embedding'))
     np.testing.assert_allclose(back, v, rtol=1e-5)
+
+
+def test_extract_cli_rejects_fbank_options_the_kernel_does_not_implement():
+    from speakerlab.bin.extract_speaker_embedding import check_fbank_config
+    base = {"FrameExtractionOptions": {"sample_freq": 16000, "frame_shift_ms": 10.0, "frame_length_ms": 25.0,
+                                       "dither": 0.0}, "MelBanksOptions": {"num_bins": 80}, "use_power": True}
+    assert check_fbank_config(base) == 80
+    import copy
+    for path, bad in ((('FrameExtractionOptions', 'sample_freq'), 8000), (('FrameExtractionOptions', 'dither'), 1.0),
+                      (('FrameExtractionOptions', 'frame_shift_ms'), 20.0), (('use_power',), False)):
+        cfg = copy.deepcopy(base)
+        node = cfg
+        for k in path[:-1]:
+            node = node[k]
+        node[path[-1]] = bad
+        with pytest.raises(ValueError):
+            check_fbank_config(cfg)
