@@ -67,6 +67,8 @@ struct ConvDesc {
   const int* rowlen = nullptr;  // ragged batches: outputs with wo >= rowlen[img] are written as 0
   int* range_flag = nullptr;    // fp16x3 range guard (below): set when an output reaches kRangeLimit
   int x1 = 0;                   // single-product fp16 MFMA (SPK_PRECISION_FP16): hi planes only
+  int wbig = 0;                 // a packed weight >= kX3WeightLimit: the tiled fp16x3 GEMM (whose
+                                // hi x hi product uses 2^11 hi_w) would overflow -> exact fp32 GEMM
   const int* run_if = nullptr;  // launch gate (below): set by launch_conv from launch_gate()
 };
 
@@ -82,6 +84,8 @@ struct ConvDesc {
 // captured behind the fp16x3 one on the same stream with its launches gated on that word
 // (launch_gate), so a flagged batch is recomputed on the device, without a host round trip.
 constexpr float kRangeLimit = 16384.0f;
+// the tiled fp16x3 GEMM scales the weights' hi plane by 2^11 (conv_gemm.hip): 31.5 * 2^11 < 65504
+constexpr float kX3WeightLimit = 31.5f;
 #ifdef __HIPCC__
 __device__ __forceinline__ void range_note(int* flag, float amax) {
   if (flag && amax >= kRangeLimit) atomicOr(flag, 1);
@@ -139,6 +143,11 @@ int conv_tile_blocks(const ConvDesc& d);
 bool halo_conv_supported(const ConvDesc& d);
 hipError_t launch_conv3x3_halo(const ConvDesc& d, hipStream_t s);
 std::string halo_kernel_name(const ConvDesc& d);
+// LDS-DMA staged fp16x3 implicit GEMM (conv_gemm_dma.hip); launch_conv routes to it
+bool gemm_dma_supported(const ConvDesc& d);
+hipError_t launch_gemm_dma(const ConvDesc& d, hipStream_t s);
+hipError_t launch_splitk_reduce(const ConvDesc& d, hipStream_t s);   // conv_gemm.hip
+std::string gemm_dma_kernel_name(const ConvDesc& d);
 // persistent short-K 1x1 GEMM (pw_gemm.hip); launch_conv routes to it
 bool pw_supported(const ConvDesc& d);
 hipError_t launch_pw(const ConvDesc& d, hipStream_t s);

@@ -74,7 +74,9 @@ __device__ __forceinline__ float epilogue_elem(const ConvDesc& d, int m, int n, 
 // ragged-row mask, i.e. no global load at all.  A persistent kernel with the next tile's
 // loads in flight needs this: a load that may be issued here (even behind a branch the
 // layer never takes) forces waits for everything issued before it (vmcnt counts in order).
-template <int TM, int TN, bool LEAN = false, bool PLAIN = false, class RowMap>
+// WIDE = true lets a wave with four accumulator tiles (the LDS-DMA GEMM's 32 x 128) take the
+// one-round-trip paths too (16 residual / AFF quads in flight).
+template <int TM, int TN, bool LEAN = false, bool PLAIN = false, bool WIDE = false, class RowMap>
 __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f32x16 (&acc)[TM][TN], int wave,
                                                int lane, int nwave, int M, RowMap rowmap,
                                                const f32x4* pre_bias = nullptr) {
@@ -102,7 +104,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
   // the wave is issued before the first use, so the whole epilogue is one memory round trip.
   constexpr int NTL = TM * TN;
   float amax = 0.f;                            // range guard (common.h)
-  if constexpr (NTL <= 2) {
+  if constexpr (NTL <= 2 || (WIDE && NTL <= 4)) {
     if (LEAN || PLAIN || (vec && !part && !d.affx && !d.gate && !d.rowbias)) {
       const int c4 = (lane & 7) * 4;
       f32x4 ra4[NTL][4];

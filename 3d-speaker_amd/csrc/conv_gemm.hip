@@ -23,6 +23,11 @@
 #include "conv_epilogue.h"
 #include "conv_loader.h"
 
+#ifndef SPK_GEXP
+#define SPK_GEXP 0   // ablation builds only (tools/gemm_exp.sh): 1 no MFMA, 2 no split, 3 no
+                     // in-loop loads, 5 no in-loop LDS stores; 0 = the product kernel
+#endif
+
 namespace spk {
 
 namespace {
@@ -160,8 +165,8 @@ conv_gemm_kernel(const ConvDesc d) {
 // fp16x3: fp32-accurate GEMM on the fp16 matrix cores (v_mfma_f32_32x32x16_f16, 16x the
 // fp32 MFMA's work per cycle).  Every operand x is split as hi = fp16(x) and
 // lo = fp16((x - hi) * 2^11) (the 2^11 keeps lo out of the fp16 subnormal range), and
-//   x * w  ~=  hi_x * hi_w  +  2^-11 * (hi_x * lo_w + lo_x * hi_w)
-// with products exact and sums in fp32 (two accumulators); the dropped lo*lo term is
+//   x * w  ~=  2^-11 * (hi_x * (2^11 hi_w)  +  hi_x * lo_w  +  lo_x * hi_w)
+// with products exact and sums in fp32 (one accumulator); the dropped lo*lo term is
 // 2^-22 relative.  Embeddings stay within the reference's own fp32-vs-fp64 noise
 // (DESIGN.md §4).  Weights are split once at model creation (misc.hip split_f16);
 // activations are split while they are staged into LDS (packed round-toward-zero
@@ -267,7 +272,12 @@ __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
         *reinterpret_cast<f16x4*>(ahi + off) = __builtin_convertvector(v, f16x4);
       } else {
         f16x4 h, l;
+#if SPK_GEXP == 2
+        h = __builtin_convertvector(v, f16x4);
+        l = h;
+#else
         split_x3(v, h, l);
+#endif
         *reinterpret_cast<f16x4*>(ahi + off) = h;
         *reinterpret_cast<f16x4*>(alo + off) = l;
       }
@@ -279,13 +289,13 @@ __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
     }
   };
 
-  f32x16 acc[TM][TN], accx[TM][TN];
+  f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; accx[i][j][r] = 0.f; }
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int li = lane & 31, lh = lane >> 5;
   auto compute = [&](int buf) {
@@ -306,15 +316,31 @@ __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
         bh[j] = *reinterpret_cast<const f16x8*>(p);
         if constexpr (!X1) bl[j] = *reinterpret_cast<const f16x8*>(p + C::PB);
       }
+      // single accumulator: the hi x hi product takes the weights' hi plane scaled by 2^11
+      // (exact: a power of two, |w| < 31.5 is checked on the host -- ConvDesc::wbig), so all
+      // three products carry the same 2^11 and sum into one accumulator, scaled back once in
+      // the epilogue (half the accumulator registers of a two-accumulator form; measured
+      // -24 % on the 128x128 tiles, which then keep two blocks per CU)
+      f16x8 bh2[TN];
+      if constexpr (!X1) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bh2[j] = bh[j] * (_Float16)2048.0f;
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+#if SPK_GEXP == 1
+          acc[i][j][0] += (float)ah[i][0] + (float)bh[j][0] + (float)al[i][1] + (float)bl[j][1];
+#else
           if constexpr (!X1) {
-            accx[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], accx[i][j], 0, 0, 0);
-            accx[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], accx[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh2[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          } else {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
           }
+#endif
         }
     }
   };
@@ -333,15 +359,23 @@ __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
     constexpr bool UNCOND = !S1 && !ADD;
     for (int kt = kt0; kt < kt1; kt += 2) {
       // even step: LDS buffer 0 holds kt, set 1 holds kt+1 (in flight), set 0 is free
+#if SPK_GEXP != 3
       load_tile(min(kt + 2, kt1 - 1), set0);
+#endif
       compute(0);
+#if SPK_GEXP != 5
       if (UNCOND || kt + 1 < kt1) store_tile(1, set1);
+#endif
       __syncthreads();
       if (kt + 1 >= kt1) break;
       // odd step: buffer 1 holds kt+1, set 0 holds kt+2 (in flight), set 1 is free
+#if SPK_GEXP != 3
       load_tile(min(kt + 3, kt1 - 1), set1);
+#endif
       compute(1);
+#if SPK_GEXP != 5
       if (UNCOND || kt + 2 < kt1) store_tile(0, set0);
+#endif
       __syncthreads();
     }
   }
@@ -349,7 +383,8 @@ __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] += accx[i][j] * (1.0f / 2048.0f);
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] *= (1.0f / 2048.0f);
   }
   epilogue_tiles<TM, TN>(d, lds, acc, wave, lane, n0 + wn * C::WTN, M, [&](int r) { return m0 + wm * C::WTM + r; });
 }
@@ -382,6 +417,19 @@ __global__ void splitk_reduce_kernel(const ConvDesc d, int M) {
   range_note(d.range_flag, amax);
 }
 
+}  // namespace
+
+// split-K combine of the partial slabs a GEMM launch left in d.partial (ksplit > 1)
+hipError_t launch_splitk_reduce(const ConvDesc& d, hipStream_t s) {
+  const int M = d.nimg * d.Ho * d.Wo;
+  const size_t total = (size_t)M * d.N;
+  const int rb = (int)std::min<size_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(rb), dim3(256), 0, s, d, M);
+  return hipGetLastError();
+}
+
+namespace {
+
 // fp16x3 split-precision MFMA (default) or exact fp32 MFMA (SPK_CONV_MFMA=f32)
 bool use_x3() {
   static const bool x3 = [] {
@@ -412,24 +460,16 @@ Cfg select_cfg(const ConvDesc& d) {
   if (d.N <= 32) return {256, 32, bk, 8, 1};
   if (d.N <= 64) return {256, 64, bk, 4, 2};
   if (M <= 4096) return {64, 128, bk, 1, 4};
-  if (use_x3() && d.wh) {
+  if (use_x3() && d.wh && !d.wbig) {
     const int t = x3_tile();
     if (t == 1) return {256, 128, 32, 4, 2};
     if (t == 2) return {128, 256, 32, 2, 4};
     if (t == 3) return {128, 128, 32, 2, 4};
-    // measured per layer (tools/gpu_ab.sh over SPK_X3_TILE): the K-concatenated shortcut
-    // GEMMs (conv3 + shortcut, AFF cat) run best on 128x256 tiles; residual epilogues with
-    // K <= 512 on 128x128 tiles, two blocks per CU, so one block's epilogue round trips
-    // overlap the other's main loop (ERes2Net-large layer3 conv3 0.68 -> 0.52 ms)
-    const bool s1 = d.s1.p != nullptr || d.s1.cin > 0;
-    const bool res = d.res != nullptr || d.ldr > 0;
-    if (s1 && d.Kp >= 256 && d.N % 256 == 0) return {128, 256, 32, 2, 4};
-    // CAM++ dense layers (BN-ReLU applied in the loader, N = 128): 128x256 as well (-6 %)
-    if (d.s0.pre_scale && d.Kp >= 256) return {128, 256, 32, 2, 4};
-    if (res && d.Kp >= 256 && d.Kp <= 512) return {128, 128, 32, 2, 4};
-    // deep K: bigger tiles halve the L2 traffic per FLOP (measured per layer)
-    if (d.Kp >= 1024 && d.N >= 512 && d.N % 256 == 0) return {128, 256, 32, 2, 4};
-    if (d.Kp >= 256) return {256, 128, 32, 4, 2};
+    // measured per layer (tools/tile_exp.sh, round 3): with one accumulator the 128x128 tile
+    // keeps two blocks (four waves per SIMD) per CU and is the fastest or within 2 % on every
+    // x3 GEMM of ERes2NetV2 / ERes2Net-large (all-128x128 27.0 ms vs 28.6 for round 2's
+    // per-layer mix); only the deepest K (the 4608-deep stage-3 downsample) keeps 256x128 (-5 %)
+    if (d.Kp >= 4096 && d.N >= 512) return {256, 128, 32, 4, 2};
   }
   // 128x128 at BK=32 still fits two blocks per CU (73.7 KB LDS): half the K-steps, twice
   // the loads in flight per step -- what the short-K 1x1 convs need
@@ -449,7 +489,7 @@ hipError_t launch_cfg(const ConvDesc& d, hipStream_t s) {
     else if (add) hipLaunchKernelGGL((conv_gemm_x1_kernel<BM, BN, WM, WN, false, true, false>), grid, block, 0, s, d);
     else if (pre) hipLaunchKernelGGL((conv_gemm_x1_kernel<BM, BN, WM, WN, false, false, true>), grid, block, 0, s, d);
     else hipLaunchKernelGGL((conv_gemm_x1_kernel<BM, BN, WM, WN, false, false, false>), grid, block, 0, s, d);
-  } else if (use_x3() && d.wh && d.wl) {
+  } else if (use_x3() && d.wh && d.wl && !d.wbig) {
     if (conv_buf_loader_ok(d, BM)) {
       if (s1) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, true, false, false, true>), grid, block, 0, s, d);
       else if (add) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, true, false, true>), grid, block, 0, s, d);
@@ -468,10 +508,7 @@ hipError_t launch_cfg(const ConvDesc& d, hipStream_t s) {
   else hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, false, false, false>), grid, block, 0, s, d);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || d.ksplit <= 1) return e;
-  const size_t total = (size_t)M * d.N;
-  const int rb = (int)std::min<size_t>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(rb), dim3(256), 0, s, d, M);
-  return hipGetLastError();
+  return launch_splitk_reduce(d, s);
 }
 
 template <int BK>
@@ -490,6 +527,7 @@ hipError_t launch_bk(const ConvDesc& d, const Cfg& c, hipStream_t s) {
 std::string conv_kernel_name(const ConvDesc& d) {
   if (halo_conv_supported(d)) return halo_kernel_name(d);
   if (use_x3() && pw_supported(d)) return pw_kernel_name(d);
+  if (gemm_dma_supported(d)) return gemm_dma_kernel_name(d);
   const Cfg c = select_cfg(d);
   const bool s1 = d.s1.p != nullptr || d.s1.cin > 0, add = d.s0.p2 != nullptr || d.s0.ld2 > 0;
   const bool pre = d.s0.pre_scale != nullptr;
@@ -497,7 +535,7 @@ std::string conv_kernel_name(const ConvDesc& d) {
                            (add ? "true" : "false") + ", " + (pre ? "true" : "false") + ">";
   if (d.x1 && d.wh && conv_buf_loader_ok(d, c.bm))
     return "conv_gemm_x1_kernel<" + std::to_string(c.bm) + ", " + std::to_string(c.bn) + ", " + tail;
-  if (use_x3() && d.wh && d.wl)
+  if (use_x3() && d.wh && d.wl && !d.wbig)
     return "conv_gemm_x3_kernel<" + std::to_string(c.bm) + ", " + std::to_string(c.bn) + ", " +
            tail.substr(0, tail.size() - 1) + (conv_buf_loader_ok(d, c.bm) ? ", true>" : ", false>");
   return "conv_gemm_kernel<" + std::to_string(c.bm) + ", " + std::to_string(c.bn) + ", " + std::to_string(c.bk) + ", " +
@@ -505,8 +543,9 @@ std::string conv_kernel_name(const ConvDesc& d) {
 }
 
 int conv_tile_blocks(const ConvDesc& d) {
-  const Cfg c = select_cfg(d);
   const int M = d.nimg * d.Ho * d.Wo;
+  if (gemm_dma_supported(d)) return ((M + 127) / 128) * ((d.N + 127) / 128);
+  const Cfg c = select_cfg(d);
   return ((M + c.bm - 1) / c.bm) * ((d.N + c.bn - 1) / c.bn);
 }
 
@@ -523,6 +562,7 @@ hipError_t launch_conv(const ConvDesc& dd, hipStream_t s) {
     return hipErrorInvalidValue;
   if (halo_conv_supported(d)) return launch_conv3x3_halo(d, s);
   if (use_x3() && pw_supported(d)) return launch_pw(d, s);
+  if (gemm_dma_supported(d)) return launch_gemm_dma(d, s);
   const Cfg c = select_cfg(d);
   return c.bk == 32 ? launch_bk<32>(d, c, s) : launch_bk<16>(d, c, s);
 }

@@ -177,6 +177,7 @@ void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const C
   d.wl = exact ? nullptr : m.dlo(p.w_off);
   const bool guard = !exact;   // producers note fp16x3 range overflows in the forward's word
   d.x1 = (!exact && m.fp16 && x1_scope) ? 1 : 0;
+  d.wbig = p.wmax >= kX3WeightLimit ? 1 : 0;
   d.bias = (use_bias && p.has_bias) ? m.dptr(p.b_off) : nullptr;
   const int M = d.nimg * d.Ho * d.Wo;
   // split-K for skinny, deep GEMMs (e.g. the 20480 -> 192 embedding layer)
