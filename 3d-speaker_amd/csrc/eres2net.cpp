@@ -139,27 +139,36 @@ struct ERes2Builder {
   // uniform lengths.
   bool fusable(const std::string& p, const T4& x, int stride, int width, int Cout, bool use_aff) const {
     const bool sc = m.has(p + ".shortcut.0.weight");
-    const bool shape = sc ? (x.C == 64 && std::getenv("SPK_NO_PROJ_FUSION") == nullptr) : x.C == 128;
-    return v2 && !use_aff && stride == 1 && scale == 2 && width <= 32 && shape && Cout == 128 &&
-           x.ld == x.C && !b.ragged && b.x3() && std::getenv("SPK_NO_BLOCK_FUSION") == nullptr;
+    const bool common = v2 && !use_aff && stride == 1 && scale == 2 && x.ld == x.C && !b.ragged && b.x3() &&
+                        std::getenv("SPK_NO_BLOCK_FUSION") == nullptr;
+    // stage 1 (res2block.hip): slices <= 32, 128 output channels, identity or 64 -> 128 projection
+    const bool s1 = width <= 32 && Cout == 128 &&
+                    (sc ? (x.C == 64 && std::getenv("SPK_NO_PROJ_FUSION") == nullptr) : x.C == 128);
+    // stage 2 (res2block_s2.hip): slices 33..64, 256 -> 256 identity
+    const bool s2 = width > 32 && width <= 64 && Cout == 256 && x.C == 256 && !sc &&
+                    std::getenv("SPK_NO_S2_FUSION") == nullptr;
+    return common && (s1 || s2);
   }
 
-  T4 fused_block(const std::string& p, const T4& x, int width, int Cout, Buf outbuf) {
+  bool fused_block(const std::string& p, const T4& x, int width, int Cout, Buf outbuf, T4& out) {
     const ChanMap xin = ChanMap::dense(x.C);
     const ChanMap om = ChanMap::dense(Cout);
-    const ChanMap sl = ChanMap::slices(width, 2, 32);
-    const ChanMap w32 = ChanMap::dense(width, 32);
+    const int sw = width <= 32 ? 32 : 64;   // padded slice width of the fused kernel
+    const ChanMap sl = ChanMap::slices(width, 2, sw);
+    const ChanMap wsw = ChanMap::dense(width, sw);
     const bool proj = m.has(p + ".shortcut.0.weight");
     const Packed& c1 = m.pack(p + ".conv1#fused", sl, {Part{p + ".conv1.weight", "", p + ".bn1", xin, 0, 0}}, x.C);
-    const Packed& ca = m.pack(p + ".convs.0#fused", w32, {Part{p + ".convs.0.weight", "", p + ".bns.0", w32, 0, 0}}, 9 * 32);
-    const Packed& cb = m.pack(p + ".convs.1#fused", w32, {Part{p + ".convs.1.weight", "", p + ".bns.1", w32, 0, 0}}, 9 * 32);
+    const Packed& ca = m.pack(p + ".convs.0#fused", wsw, {Part{p + ".convs.0.weight", "", p + ".bns.0", wsw, 0, 0}}, 9 * sw);
+    const Packed& cb = m.pack(p + ".convs.1#fused", wsw, {Part{p + ".convs.1.weight", "", p + ".bns.1", wsw, 0, 0}}, 9 * sw);
     std::vector<Part> parts3{Part{p + ".conv3.weight", "", p + ".bn3", sl, 0, 0}};
-    if (proj) parts3.push_back(Part{p + ".shortcut.0.weight", "", p + ".shortcut.1", xin, 0, 64});
-    const Packed& c3 = m.pack(p + ".conv3#fused", om, parts3, 64 + (proj ? x.C : 0));
+    if (proj) parts3.push_back(Part{p + ".shortcut.0.weight", "", p + ".shortcut.1", xin, 0, 2 * sw});
+    const Packed& c3 = m.pack(p + ".conv3#fused", om, parts3, 2 * sw + (proj ? x.C : 0));
+    // the stage-2 kernel's 3x3 convs use the one-accumulator fp16x3 form (hi_w scaled by 2^11)
+    if (sw == 64 && (ca.wmax >= kX3WeightLimit || cb.wmax >= kX3WeightLimit)) return false;
     const double px = (double)x.H * x.W;
     b.macs_per_utt += px * x.C * (double)width * 2 + 2.0 * px * 9.0 * width * width + px * (double)width * 2 * Cout +
                       (proj ? px * x.C * (double)Cout : 0.0);
-    T4 out{outbuf, Cout, x.H, x.W, Cout};
+    out = T4{outbuf, Cout, x.H, x.W, Cout};
     if (b.plan) {
       Res2Desc d;
       d.nimg = b.B; d.H = x.H; d.W = x.W; d.C = x.C; d.width = width;
@@ -178,13 +187,14 @@ struct ERes2Builder {
         return launch_res2_block(d, c.stream);
       }, res2_block_kernel_name(d), bytes);
     }
-    return out;
+    return true;
   }
 
   T4 block(const std::string& p, const T4& x, int stride, int width, int planes, bool use_aff, Buf outbuf) {
     const int Ho = (x.H - 1) / stride + 1, Wo = (x.W - 1) / stride + 1;
     const int Cout = planes * expansion;
-    if (fusable(p, x, stride, width, Cout, use_aff)) return fused_block(p, x, width, Cout, outbuf);
+    T4 fo;
+    if (fusable(p, x, stride, width, Cout, use_aff) && fused_block(p, x, width, Cout, outbuf, fo)) return fo;
     const ChanMap sl = ChanMap::slices(width, scale);
     const int wp = sl.n_phys / scale;
     const int ldt = sl.n_phys;

@@ -18,7 +18,7 @@ struct Res2Desc {
   int Cout = 0;                 // output channels (0: C)
   bool proj = false;            // 1x1 projection shortcut + BN (ERes2NetV2.py:84-88), packed
                                 // into w3 as K columns 64 .. 64+C, its BN shift into b3
-  int width = 0;                // Res2Net slice width (26 for ERes2NetV2 layer1), <= 32
+  int width = 0;                // Res2Net slice width (26 for ERes2NetV2 layer1, 52 for layer2), <= 64
   // fp16 hi / lo planes of the BN-folded packed weights (Model::pack) and fp32 biases:
   const uint16_t* w1h = nullptr; const uint16_t* w1l = nullptr; const float* b1 = nullptr;   // [64][C]
   const uint16_t* wah = nullptr; const uint16_t* wal = nullptr; const float* ba = nullptr;   // convs.0 [32][9*32]
@@ -29,6 +29,9 @@ struct Res2Desc {
 };
 
 bool res2_block_supported(const Res2Desc& d);
+// stage-2 identity blocks (256 -> 256, slices 33..64 wide): res2block_s2.hip
+bool res2_block_s2_supported(const Res2Desc& d);
+hipError_t launch_res2_block_s2(const Res2Desc& d, hipStream_t s);
 hipError_t launch_res2_block(const Res2Desc& d, hipStream_t s);
 std::string res2_block_kernel_name(const Res2Desc& d);
 

@@ -479,6 +479,7 @@ int device_cus_r2() {
 }  // namespace
 
 bool res2_block_supported(const Res2Desc& d) {
+  if (res2_block_s2_supported(d)) return true;
   const int co = d.Cout ? d.Cout : d.C;
   const bool shape = d.proj ? (d.C == 64 && co == 128) : (d.C == 128 && co == 128);
   return conv_use_x3() && shape && d.width >= 1 && d.width <= 32 && d.nimg > 0 && d.H > 0 && d.W > 0 &&
@@ -486,10 +487,12 @@ bool res2_block_supported(const Res2Desc& d) {
 }
 
 std::string res2_block_kernel_name(const Res2Desc& d) {
+  if (res2_block_s2_supported(d)) return "res2_block_s2_kernel";
   return d.proj ? "res2_block_kernel<64, 128, true>" : "res2_block_kernel<128, 128, false>";
 }
 
 hipError_t launch_res2_block(const Res2Desc& d, hipStream_t s) {
+  if (res2_block_s2_supported(d)) return launch_res2_block_s2(d, s);
   if (!res2_block_supported(d) || d.x == d.out) return hipErrorInvalidValue;
   const int ntiles = d.nimg * ((d.W + 15) / 16) * ((d.H + 7) / 8);
   int grid = std::min(device_cus_r2(), (ntiles + 7) / 8 * 8);

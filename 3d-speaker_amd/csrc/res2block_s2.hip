@@ -1,0 +1,501 @@
+// Fused ERes2NetV2 Res2Net block (speakerlab/models/eres2net/ERes2NetV2.py:65-91) for the
+// stage-2 identity blocks (256 -> 256 channels, width 52, scale 2): one persistent kernel,
+// fp16x3 MFMA, gfx950.  VERDICT r2 "next" item 2: unfused, a stage-2 block is four launches
+// (conv1 GEMM, two halo 3x3 convs, the persistent conv3 + residual) whose intermediates make
+// full HBM round trips (~5 KB per pixel for 2 KB of real input and output).
+//
+// Same structure as the stage-1 kernel (res2block.hip) -- an 8 x 16 output tile per
+// workgroup, everything between block input and output in LDS as fp16 hi / lo planes,
+// transposed 16x16x32 MFMAs (weights = A, each lane gets four output channels of one pixel)
+// -- with what the wider block needs:
+//   * slices padded 52 -> 64 channels (zero weights and bias: the padding holds Hardtanh(0)
+//     = 0); conv1 N = 128 (eight 16-channel n-tiles, one per wave, its 8 k-steps of A
+//     fragments resident in VGPRs), conv3 K = 128;
+//   * the two 3x3 weight matrices (2 x 147 KB as hi / lo) do not fit in LDS next to the
+//     tiles: each wave streams its n-tile's A fragments straight from global memory (every
+//     workgroup reads the same 295 KB: L2-resident), one tap ahead, with no barrier in the
+//     tap loop;
+//   * conv3's A fragments are loaded per tile at the start of the conv3 phase (their VGPRs
+//     are free then), its residual one pixel tile ahead;
+//   * conv1 input chunks of 16 pixels x 256 channels, staged in two LDS buffers, their global
+//     loads three chunks ahead in a register ring that crosses tiles.
+// LDS (halves): R0 = S0 [240 px][64] (halo-2 region, slice 0) or CAT [128 px][128], SP
+// [180 px][64] (halo-1 region, slice 1 -> sp = y0 + s1 in place), XC [2][16 px][256]; rows
+// XOR-swizzled per 16-byte chunk (64-channel rows: chunk ^ (px & 7); 128 / 256-channel rows:
+// chunk ^ (px & 15)), so every fragment read and epilogue write is bank-conflict free.
+// Halo recompute: conv1 runs on 240 pixels and convs.0 on 180 per 128 outputs.
+#include <algorithm>
+#include <type_traits>
+
+#include "conv_epilogue.h"
+#include "res2block.h"
+
+#ifndef SPK_S2_PROF
+#define SPK_S2_PROF 0
+#endif
+#ifndef SPK_S2_EXP
+#define SPK_S2_EXP 0   // ablation builds only (tools/build_s2prof.sh)
+#endif
+
+namespace spk {
+
+#if SPK_S2_PROF
+// diagnostic build only (tools/s2_prof.py): per-wave cycle counts of the kernel's phases,
+// stored by every lane to its own slot (vector stores)
+constexpr int S2P_PH = 10, S2P_BLK = 256;
+__device__ long long s2_prof_buf[S2P_BLK * 8 * S2P_PH * 64];
+#endif
+
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct S2 {
+  static constexpr int NT = 512;
+  static constexpr int CI = 256, CO = 256, SW = 64;                 // channels; padded slice width
+  static constexpr int TH = 8, TW = 16;
+  static constexpr int RH = TH + 4, RW = TW + 4, NR = RH * RW;      // S0 region 12 x 20 = 240 px
+  static constexpr int PH = TH + 2, PW = TW + 2, NP = PH * PW;      // SP region 10 x 18 = 180 px
+  static constexpr int NO = TH * TW;                                // 128 output px
+  static constexpr int XCH = 16, NCH = NR / XCH;                    // 15 conv1 chunks of 16 px
+  static constexpr int XF = XCH * (CI / 4) / NT;                    // 2 float4 per thread per chunk
+  static constexpr int KS1 = CI / 32;                               // conv1 k-steps (8)
+  static constexpr int K3 = 2 * SW;                                 // conv3 K (CAT: 128)
+  static constexpr int KS3 = K3 / 32;                               // 4
+  static constexpr int KW = 9 * SW;                                 // 3x3 packed row length (576)
+  static constexpr int S0_PL = NR * SW, CAT_PL = NO * K3;           // plane sizes (halves)
+  static constexpr int R0_PL = S0_PL > CAT_PL ? S0_PL : CAT_PL;
+  static constexpr int SP_PL = NP * SW, XC_PL = XCH * CI;
+  static constexpr int OFF_SP = 2 * R0_PL, OFF_XC = OFF_SP + 2 * SP_PL;
+  static constexpr int LDS_HALVES = OFF_XC + 4 * XC_PL;
+  static_assert(NR % XCH == 0 && XCH * (CI / 4) % NT == 0, "conv1 chunking");
+  static_assert(2 * LDS_HALVES <= 160 * 1024, "LDS");
+};
+
+__device__ __forceinline__ float htanh(float v) { return fminf(fmaxf(v, 0.0f), 20.0f); }
+__device__ __forceinline__ f32x4 mfma16(const f16x8& a, const f16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f16x8 ld8(const uint16_t* p) { return *reinterpret_cast<const f16x8*>(p); }
+
+__global__ void __launch_bounds__(512, 1)
+res2_block_s2_kernel(const Res2Desc d) {
+  using G = S2;
+  __shared__ __attribute__((aligned(16))) _Float16 lds[G::LDS_HALVES];
+  _Float16* const S0h = lds;                  // S0 region, then (aliased) CAT
+  _Float16* const S0l = lds + G::S0_PL;
+  _Float16* const CATh = lds;
+  _Float16* const CATl = lds + G::CAT_PL;
+  _Float16* const SPh = lds + G::OFF_SP;
+  _Float16* const SPl = SPh + G::SP_PL;
+  _Float16* const XCh = lds + G::OFF_XC;     // [buf][plane][px][256]
+  constexpr int CI = G::CI, SW = G::SW;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // re-derived per tile from an opaque copy of the lane id (below): otherwise the compiler
+  // hoists every lane-dependent address of all four phases out of the tile loop and keeps
+  // them live (spilled) across it
+  int l16 = lane & 15, lq = lane >> 4;
+  const int H = d.H, W = d.W;
+  const int ntx = (W + G::TW - 1) / G::TW, nty = (H + G::TH - 1) / G::TH;
+  const int ntiles = d.nimg * ntx * nty;
+#if SPK_S2_PROF
+  long long tp[S2P_PH] = {};
+  long long tl = __builtin_amdgcn_s_memtime();
+#define S2_STAMP(i) do { const long long now_ = __builtin_amdgcn_s_memtime(); tp[i] += now_ - tl; tl = now_; } while (0)
+#else
+#define S2_STAMP(i) do {} while (0)
+#endif
+
+  const f32x4 b1v = *reinterpret_cast<const f32x4*>(d.b1 + 16 * wave + 4 * lq);
+  const int ntc = wave & 3;                   // 3x3 convs: 16-channel n-tile of the 64
+  const int pg = wave >> 2;                   //   and pixel-tile parity
+  const f32x4 bav = *reinterpret_cast<const f32x4*>(d.ba + 16 * ntc + 4 * lq);
+  const f32x4 bbv = *reinterpret_cast<const f32x4*>(d.bb + 16 * ntc + 4 * lq);
+  constexpr float kLo = 1.0f / 2048.0f;
+  // 3x3 weight fragments of this lane: row 16 ntc + l16, k = 64 tap + 32 kk + 8 lq
+  size_t wrow = 0;
+
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
+  const int per = (ntiles + 7) / 8;
+  const int t_lo = xcd * per, t_hi = min(ntiles, t_lo + per);
+  auto load_chunk = [&](int ch, f32x4 (&v)[G::XF], int ty0, int tx0, const float* im) {
+#pragma unroll
+    for (int j = 0; j < G::XF; ++j) {
+      const int i = tid + G::NT * j;
+      const int px = ch * G::XCH + i / (CI / 4), q = i % (CI / 4);
+      const int gy = min(max(ty0 - 2 + px / G::RW, 0), H - 1);
+      const int gx = min(max(tx0 - 2 + px % G::RW, 0), W - 1);
+      v[j] = *reinterpret_cast<const f32x4*>(im + ((size_t)gy * W + gx) * CI + 4 * q);
+    }
+  };
+  auto store_chunk = [&](const f32x4 (&v)[G::XF], int buf) {
+#pragma unroll
+    for (int j = 0; j < G::XF; ++j) {
+      const int i = tid + G::NT * j;
+      const int px = i / (CI / 4), q = i % (CI / 4);
+      const int a = buf * 2 * G::XC_PL + px * CI + 8 * ((q >> 1) ^ (px & 15)) + 4 * (q & 1);
+      h16x4 h, l;
+      split_x3(v[j], h, l);
+      *reinterpret_cast<h16x4*>(XCh + a) = h;
+      *reinterpret_cast<h16x4*>(XCh + G::XC_PL + a) = l;
+    }
+  };
+  auto tile_origin = [&](int tt, int& im, int& ty0, int& tx0) {
+    im = tt / (ntx * nty);
+    ty0 = ((tt / ntx) % nty) * G::TH;
+    tx0 = (tt % ntx) * G::TW;
+  };
+  // 3x3 conv over NPT pixel tiles of this wave: pixel tile p = pg + 2 i covers 16 region
+  // pixels whose 3x3 windows start at base[i] (row length RL) in the source plane (hi at src,
+  // lo at src + SRC_PL); A fragments streamed from global memory one tap ahead
+  auto conv3x3 = [&](auto npt_c, const int (&base)[decltype(npt_c)::value], const _Float16* src, int src_pl, int rl,
+                     const uint16_t* wh, const uint16_t* wl, f32x4 (&acc)[decltype(npt_c)::value]) {
+    constexpr int NPT = decltype(npt_c)::value;
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // one accumulator (conv_gemm.hip's form): the hi x hi product takes the weights' hi
+    // fragment scaled by 2^11 (exact; |w| < kX3WeightLimit is checked on the host), so the
+    // three products share one scale and one accumulator, scaled back at the end.
+    // A fragments ping-pong between two register sets: a tap's MFMAs read one set while the
+    // next tap's loads land in the other (no register copy, which would wait for the loads);
+    // the scheduling barriers keep the compiler from sinking the loads next to their use
+    f16x8 wa[2][2][2];          // [set][hi / lo][kk]
+    auto wload = [&](int tap, f16x8 (&w)[2][2]) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#if SPK_S2_EXP == 1
+        w[0][kk] = ld8(wh + wrow + 32 * kk);   // experiment: every tap reads tap 0 (L1 hits)
+        w[1][kk] = ld8(wl + wrow + 32 * kk);
+#else
+        w[0][kk] = ld8(wh + wrow + 64 * tap + 32 * kk);
+        w[1][kk] = ld8(wl + wrow + 64 * tap + 32 * kk);
+#endif
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto taps = [&](int tap, const f16x8 (&w)[2][2]) {
+      const int ty = tap / 3;
+      const int toff = ty * rl + (tap - 3 * ty);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        // all of the k-step's B fragments requested before its first MFMA (the LDS latency
+        // of each read is otherwise exposed in front of its own three MFMAs)
+        f16x8 bh[NPT], bl[NPT];
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+          const int px = base[i] + toff;
+          const int a = px * SW + 8 * ((4 * kk + lq) ^ (px & 7));
+          bh[i] = *reinterpret_cast<const f16x8*>(src + a);
+          bl[i] = *reinterpret_cast<const f16x8*>(src + src_pl + a);
+        }
+        const f16x8 w2 = w[0][kk] * (_Float16)2048.0f;
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) acc[i] = mfma16(w2, bh[i], acc[i]);
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) acc[i] = mfma16(w[0][kk], bl[i], acc[i]);
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) acc[i] = mfma16(w[1][kk], bh[i], acc[i]);
+      }
+    };
+    wload(0, wa[0]);
+#pragma unroll 1
+    for (int tap = 0; tap < 8; tap += 2) {
+      wload(tap + 1, wa[1]);
+      taps(tap, wa[0]);
+      wload(tap + 2, wa[0]);
+      taps(tap + 1, wa[1]);
+    }
+    taps(8, wa[0]);
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) acc[i] *= kLo;
+  };
+
+  // One continuous stream of conv1 input chunks over the block's tiles: chunk k of a tile sits
+  // in register-ring slot k % 3 (15 chunks per tile, so the next tile continues the pattern)
+  // and is staged into LDS buffer xb ^ (k & 1), xb alternating per tile.  Invariant at the
+  // top of a tile: chunk 0 is in LDS buffer xb, chunks 1..3 are in flight in the ring.
+  f32x4 pf[3][G::XF];
+  int xb = 0;
+  if (t_lo + slot < t_hi) {
+    int im, ty0, tx0;
+    tile_origin(t_lo + slot, im, ty0, tx0);
+    const float* p0 = d.x + (size_t)im * H * W * CI;
+    load_chunk(0, pf[0], ty0, tx0, p0);
+    load_chunk(1, pf[1], ty0, tx0, p0);
+    load_chunk(2, pf[2], ty0, tx0, p0);
+    store_chunk(pf[0], 0);
+    load_chunk(3, pf[0], ty0, tx0, p0);
+  }
+  for (int t = t_lo + slot; t < t_hi; t += nslot) {
+    {
+      int ln;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+      l16 = ln & 15;
+      lq = ln >> 4;
+    }
+    wrow = (size_t)(16 * ntc + l16) * G::KW + 8 * lq;
+    int img, y0, x0;
+    tile_origin(t, img, y0, x0);
+    const float* const xim = d.x + (size_t)img * H * W * CI;
+    int nimg_, ny0, nx0;                      // the next tile (the last tile re-reads itself)
+    tile_origin(t + nslot < t_hi ? t + nslot : t, nimg_, ny0, nx0);
+    const float* const nim = d.x + (size_t)nimg_ * H * W * CI;
+
+    // ================= 1. conv1 on the S0 region, one 16-pixel chunk per step: wave w
+    //   computes its n-tile (channels 16w .. 16w+15 of the two slices) for the chunk; its A
+    //   fragments are (re)loaded per tile (L2-resident; their VGPRs serve the 3x3 phase)
+    f16x8 a1h[G::KS1], a1l[G::KS1];
+#pragma unroll
+    for (int ks = 0; ks < G::KS1; ++ks) {
+      const size_t o = (size_t)(16 * wave + l16) * CI + 32 * ks + 8 * lq;
+      a1h[ks] = ld8(d.w1h + o);
+      a1l[ks] = ld8(d.w1l + o);
+    }
+#pragma unroll 1
+    for (int c3 = 0; c3 < G::NCH; c3 += 3) {
+#pragma unroll
+    for (int cj = 0; cj < 3; ++cj) {
+      const int ch = c3 + cj;
+      S2_STAMP(2);
+      __syncthreads();
+      S2_STAMP(0);
+      // stage chunk ch + 1 (for ch = 14: the next tile's chunk 0), then request chunk ch + 4
+      // (this tile's, or the next tile's ch - 11) into the slot it leaves
+      store_chunk(pf[(cj + 1) % 3], xb ^ ((ch + 1) & 1));
+      {
+        const int cn = ch + 4;
+        const bool nx = cn >= G::NCH;
+        load_chunk(nx ? cn - G::NCH : cn, pf[(cj + 1) % 3], nx ? ny0 : y0, nx ? nx0 : x0, nx ? nim : xim);
+      }
+      S2_STAMP(1);
+      const _Float16* xh = XCh + (xb ^ (ch & 1)) * 2 * G::XC_PL;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accx = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k4 = 0; k4 < G::KS1; k4 += 4) {
+        f16x8 bh[4], bl[4];                     // four k-steps' B fragments in flight at once
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int a = l16 * CI + 8 * ((4 * (k4 + u) + lq) ^ l16);
+          bh[u] = *reinterpret_cast<const f16x8*>(xh + a);
+          bl[u] = *reinterpret_cast<const f16x8*>(xh + G::XC_PL + a);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          acc = mfma16(a1h[k4 + u], bh[u], acc);
+          accx = mfma16(a1h[k4 + u], bl[u], accx);
+          accx = mfma16(a1l[k4 + u], bh[u], accx);
+        }
+      }
+      const int rpx = ch * G::XCH + l16;       // S0-region pixel of this lane's column
+      const int r = rpx / G::RW, c = rpx % G::RW;
+      const int gy = y0 - 2 + r, gx = x0 - 2 + c;
+      const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;   // conv padding: zero outside
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = in ? htanh(acc[e] + accx[e] * kLo + b1v[e]) : 0.f;
+      h16x4 h, l;
+      split_x3(v, h, l);
+      const int cc = 16 * (wave & 3) + 4 * lq;  // channel within the slice
+      const int kb = cc >> 3, sub = cc & 7;
+      if (wave < 4) {
+        const int a = rpx * SW + 8 * (kb ^ (rpx & 7)) + sub;
+        *reinterpret_cast<h16x4*>(S0h + a) = h;
+        *reinterpret_cast<h16x4*>(S0l + a) = l;
+      } else if (r >= 1 && r <= G::PH && c >= 1 && c <= G::PW) {
+        const int sp = (r - 1) * G::PW + (c - 1);
+        const int a = sp * SW + 8 * (kb ^ (sp & 7)) + sub;
+        *reinterpret_cast<h16x4*>(SPh + a) = h;
+        *reinterpret_cast<h16x4*>(SPl + a) = l;
+      }
+    }
+    }
+    xb ^= 1;                                  // 15 chunks per tile: the next tile's chunk 0 is in xb ^ 1
+    S2_STAMP(2);
+    __syncthreads();
+    S2_STAMP(3);
+
+    // ================= 2. convs.0 on the SP region (6 pixel tiles per wave)
+    const int cc = 16 * ntc + 4 * lq, kbo = cc >> 3, subo = cc & 7;
+    f32x4 y[6];
+    {
+      int base[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int p = min(16 * (pg + 2 * i) + l16, G::NP - 1);
+        base[i] = (p / G::PW) * G::RW + p % G::PW;
+      }
+      conv3x3(std::integral_constant<int, 6>{}, base, S0h, G::S0_PL, G::RW, d.wah, d.wal, y);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int p = 16 * (pg + 2 * i) + l16;
+        const int gy = y0 - 1 + p / G::PW, gx = x0 - 1 + p % G::PW;
+        const bool in = p < G::NP && gy >= 0 && gy < H && gx >= 0 && gx < W;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[i][e] = in ? htanh(y[i][e] + bav[e]) : 0.f;
+      }
+    }
+    S2_STAMP(4);
+    __syncthreads();                          // S0 reads done: the region becomes CAT
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int p = 16 * (pg + 2 * i) + l16;
+      if (p >= G::NP) continue;
+      const int a = p * SW + 8 * (kbo ^ (p & 7)) + subo;
+      const h16x4 sh = *reinterpret_cast<const h16x4*>(SPh + a);
+      const h16x4 sl = *reinterpret_cast<const h16x4*>(SPl + a);
+      f32x4 sp;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sp[e] = y[i][e] + ((float)sh[e] + (float)sl[e] * kLo);
+      h16x4 h, l;
+      split_x3(sp, h, l);
+      *reinterpret_cast<h16x4*>(SPh + a) = h;
+      *reinterpret_cast<h16x4*>(SPl + a) = l;
+      const int r = p / G::PW - 1, c = p % G::PW - 1;
+      if (r >= 0 && r < G::TH && c >= 0 && c < G::TW) {
+        const int o = r * G::TW + c;
+        const int ao = o * G::K3 + 8 * (kbo ^ (o & 15)) + subo;
+        split_x3(y[i], h, l);
+        *reinterpret_cast<h16x4*>(CATh + ao) = h;
+        *reinterpret_cast<h16x4*>(CATl + ao) = l;
+      }
+    }
+    __syncthreads();
+
+    S2_STAMP(5);
+    // ================= 3. convs.1 on the output tile (4 pixel tiles per wave)
+    {
+      int base[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int o = 16 * (pg + 2 * i) + l16;
+        base[i] = (o / G::TW) * G::PW + o % G::TW;
+      }
+      f32x4 z[4];
+      conv3x3(std::integral_constant<int, 4>{}, base, SPh, G::SP_PL, G::PW, d.wbh, d.wbl, z);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int o = 16 * (pg + 2 * i) + l16;
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = htanh(z[i][e] + bbv[e]);
+        h16x4 h, l;
+        split_x3(v, h, l);
+        const int ao = o * G::K3 + 8 * ((8 + kbo) ^ (o & 15)) + subo;   // CAT channels 64..127
+        *reinterpret_cast<h16x4*>(CATh + ao) = h;
+        *reinterpret_cast<h16x4*>(CATl + ao) = l;
+      }
+    }
+    S2_STAMP(6);
+    // conv3 A fragments (this wave's n-tiles wave and wave + 8) and biases: the 3x3 phase's
+    // registers are free now; requested before the barrier so they land during it
+    f16x8 a3h[2][G::KS3], a3l[2][G::KS3];
+    f32x4 b3v[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = 16 * (wave + 8 * j);
+#pragma unroll
+      for (int ks = 0; ks < G::KS3; ++ks) {
+        const size_t o = (size_t)(n + l16) * G::K3 + 32 * ks + 8 * lq;
+        a3h[j][ks] = ld8(d.w3h + o);
+        a3l[j][ks] = ld8(d.w3l + o);
+      }
+      b3v[j] = *reinterpret_cast<const f32x4*>(d.b3 + n + 4 * lq);
+    }
+    __syncthreads();
+    S2_STAMP(7);
+
+    // ================= 4. conv3 + bn3 + residual + Hardtanh -> out (8 pixel tiles, each with
+    //   the wave's two n-tiles); the residual one pixel tile ahead
+    auto res_load = [&](int pt, f32x4 (&r)[2]) {
+      const int gy = min(y0 + pt, H - 1), gx = min(x0 + l16, W - 1);
+      const float* rp = xim + ((size_t)gy * W + gx) * CI + 4 * lq;
+      r[0] = *reinterpret_cast<const f32x4*>(rp + 16 * wave);
+      r[1] = *reinterpret_cast<const f32x4*>(rp + 16 * (wave + 8));
+    };
+    f32x4 res[2][2];
+    res_load(0, res[0]);
+#pragma unroll 1
+    for (int p2 = 0; p2 < 8; p2 += 2) {
+#pragma unroll
+    for (int pj = 0; pj < 2; ++pj) {
+      const int pt = p2 + pj;
+      res_load(min(pt + 1, 7), res[pj ^ 1]);   // unconditional (the last re-reads itself)
+      const int o = 16 * pt + l16;
+      f32x4 acc[2], accx[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) { acc[j] = f32x4{0.f, 0.f, 0.f, 0.f}; accx[j] = acc[j]; }
+      f16x8 bh[G::KS3], bl[G::KS3];             // the pixel tile's whole K in flight at once
+#pragma unroll
+      for (int ks = 0; ks < G::KS3; ++ks) {
+        const int a = o * G::K3 + 8 * ((4 * ks + lq) ^ (o & 15));
+        bh[ks] = *reinterpret_cast<const f16x8*>(CATh + a);
+        bl[ks] = *reinterpret_cast<const f16x8*>(CATl + a);
+      }
+#pragma unroll
+      for (int ks = 0; ks < G::KS3; ++ks) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[j] = mfma16(a3h[j][ks], bh[ks], acc[j]);
+          accx[j] = mfma16(a3h[j][ks], bl[ks], accx[j]);
+          accx[j] = mfma16(a3l[j][ks], bh[ks], accx[j]);
+        }
+      }
+      const int gy = y0 + pt, gx = x0 + l16;
+      if (gy < H && gx < W) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int n = 16 * (wave + 8 * j) + 4 * lq;
+          f32x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = htanh(acc[j][e] + accx[j][e] * kLo + b3v[j][e] + res[pj][j][e]);
+          *reinterpret_cast<f32x4*>(d.out + (((size_t)img * H + gy) * W + gx) * G::CO + n) = v;
+        }
+      }
+    }
+    }
+    S2_STAMP(8);
+    __syncthreads();                          // CAT reads done before the next tile's conv1
+    S2_STAMP(9);
+  }
+#if SPK_S2_PROF
+  if (blockIdx.x < S2P_BLK)
+    for (int i = 0; i < S2P_PH; ++i) s2_prof_buf[(((size_t)blockIdx.x * 8 + wave) * S2P_PH + i) * 64 + lane] = tp[i];
+#endif
+}
+
+int device_cus_s2() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 256;
+  return n;
+}
+
+}  // namespace
+
+bool res2_block_s2_supported(const Res2Desc& d) {
+  const int co = d.Cout ? d.Cout : d.C;
+  return conv_use_x3() && !d.proj && d.C == 256 && co == 256 && d.width > 32 && d.width <= 64 && d.nimg > 0 &&
+         d.H > 0 && d.W > 0 && d.w1h && d.w1l && d.wah && d.wal && d.wbh && d.wbl && d.w3h && d.w3l && d.b1 && d.ba &&
+         d.bb && d.b3;
+}
+
+hipError_t launch_res2_block_s2(const Res2Desc& d, hipStream_t s) {
+  if (!res2_block_s2_supported(d) || d.x == d.out) return hipErrorInvalidValue;
+  const int ntiles = d.nimg * ((d.W + 15) / 16) * ((d.H + 7) / 8);
+  int grid = std::min(device_cus_s2(), (ntiles + 7) / 8 * 8);
+  grid = std::max(8, grid / 8 * 8);
+  hipLaunchKernelGGL(res2_block_s2_kernel, dim3(grid), dim3(512), 0, s, d);
+  return hipGetLastError();
+}
+
+}  // namespace spk
+
+#if SPK_S2_PROF
+extern "C" int spk_exp_s2_prof(long long* host, size_t n) {
+  const size_t all = sizeof(spk::s2_prof_buf) / sizeof(long long);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(spk::s2_prof_buf), std::min(n, all) * sizeof(long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

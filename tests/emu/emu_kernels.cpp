@@ -207,59 +207,61 @@ bool conv_use_x3() {
   return !(e && std::string(e) == "f32");
 }
 
-// fused Res2Net block (res2block.hip), the kernel's contract in double precision:
-// conv1 + bn1 + Hardtanh -> s0 | s1 (32-channel slices), y0 = Ht(conv3x3(s0)),
-// y1 = Ht(conv3x3(y0 + s1)), out = Ht(conv3(cat(y0, y1)) + x) -- or, with the projection
-// shortcut, Ht(conv3(cat(y0, y1, x))) -- zero padding at the edges
+// fused Res2Net block (res2block.hip, res2block_s2.hip), the kernels' contract in double
+// precision: conv1 + bn1 + Hardtanh -> s0 | s1 (slices padded to SW = 32 or 64 channels),
+// y0 = Ht(conv3x3(s0)), y1 = Ht(conv3x3(y0 + s1)), out = Ht(conv3(cat(y0, y1)) + x) -- or,
+// with the projection shortcut, Ht(conv3(cat(y0, y1, x))) -- zero padding at the edges
 bool res2_block_supported(const Res2Desc& d) {
   const int co = d.Cout ? d.Cout : d.C;
-  const bool shape = d.proj ? (d.C == 64 && co == 128) : (d.C == 128 && co == 128);
-  return shape && d.width >= 1 && d.width <= 32 && d.w1 && d.wa && d.wb && d.w3 && d.b1 && d.ba && d.bb && d.b3;
+  const bool s1 = (d.proj ? (d.C == 64 && co == 128) : (d.C == 128 && co == 128)) && d.width >= 1 && d.width <= 32;
+  const bool s2 = !d.proj && d.C == 256 && co == 256 && d.width > 32 && d.width <= 64;
+  return (s1 || s2) && d.w1 && d.wa && d.wb && d.w3 && d.b1 && d.ba && d.bb && d.b3;
 }
 std::string res2_block_kernel_name(const Res2Desc& d) { return "emu_res2_block<" + std::to_string(d.C) + ">"; }
 hipError_t launch_res2_block(const Res2Desc& d, hipStream_t) {
   EMU_GATE();
   if (!res2_block_supported(d) || d.x == d.out) return hipErrorInvalidValue;
-  const int H = d.H, W = d.W, C = d.C, CO = d.Cout ? d.Cout : d.C, K3 = d.proj ? 64 + C : 64;
+  const int SW = d.width <= 32 ? 32 : 64;
+  const int H = d.H, W = d.W, C = d.C, CO = d.Cout ? d.Cout : d.C, K3 = d.proj ? 2 * SW + C : 2 * SW;
   auto ht = [](double v) { return std::min(std::max(v, 0.0), 20.0); };
-  std::vector<double> t1((size_t)H * W * 64), y0((size_t)H * W * 32), sp((size_t)H * W * 32), y1((size_t)H * W * 32);
+  std::vector<double> t1((size_t)H * W * 2 * SW), y0((size_t)H * W * SW), sp((size_t)H * W * SW), y1((size_t)H * W * SW);
   auto conv3 = [&](const std::vector<double>& in, const float* w, const float* b, std::vector<double>& out) {
     for (int y = 0; y < H; ++y)
       for (int x = 0; x < W; ++x)
-        for (int n = 0; n < 32; ++n) {
+        for (int n = 0; n < SW; ++n) {
           double acc = b[n];
           for (int tap = 0; tap < 9; ++tap) {
             const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
             if (yy < 0 || yy >= H || xx < 0 || xx >= W) continue;
-            const double* iv = &in[((size_t)yy * W + xx) * 32];
-            for (int c = 0; c < 32; ++c) acc += (double)w[(size_t)n * 288 + tap * 32 + c] * iv[c];
+            const double* iv = &in[((size_t)yy * W + xx) * SW];
+            for (int c = 0; c < SW; ++c) acc += (double)w[(size_t)n * 9 * SW + tap * SW + c] * iv[c];
           }
-          out[((size_t)y * W + x) * 32 + n] = ht(acc);
+          out[((size_t)y * W + x) * SW + n] = ht(acc);
         }
   };
   for (int img = 0; img < d.nimg; ++img) {
     const float* xi = d.x + (size_t)img * H * W * C;
     float* oi = d.out + (size_t)img * H * W * CO;
     for (size_t p = 0; p < (size_t)H * W; ++p)
-      for (int n = 0; n < 64; ++n) {
+      for (int n = 0; n < 2 * SW; ++n) {
         double acc = d.b1[n];
         for (int k = 0; k < C; ++k) acc += (double)d.w1[(size_t)n * C + k] * xi[p * C + k];
-        t1[p * 64 + n] = ht(acc);
+        t1[p * 2 * SW + n] = ht(acc);
       }
-    std::vector<double> s0((size_t)H * W * 32);
+    std::vector<double> s0((size_t)H * W * SW);
     for (size_t p = 0; p < (size_t)H * W; ++p)
-      for (int c = 0; c < 32; ++c) s0[p * 32 + c] = t1[p * 64 + c];
+      for (int c = 0; c < SW; ++c) s0[p * SW + c] = t1[p * 2 * SW + c];
     conv3(s0, d.wa, d.ba, y0);
     for (size_t p = 0; p < (size_t)H * W; ++p)
-      for (int c = 0; c < 32; ++c) sp[p * 32 + c] = y0[p * 32 + c] + t1[p * 64 + 32 + c];
+      for (int c = 0; c < SW; ++c) sp[p * SW + c] = y0[p * SW + c] + t1[p * 2 * SW + SW + c];
     conv3(sp, d.wb, d.bb, y1);
     for (size_t p = 0; p < (size_t)H * W; ++p)
       for (int n = 0; n < CO; ++n) {
         double acc = d.b3[n] + (d.proj ? 0.0 : xi[p * C + n]);
-        for (int c = 0; c < 32; ++c)
-          acc += (double)d.w3[(size_t)n * K3 + c] * y0[p * 32 + c] + (double)d.w3[(size_t)n * K3 + 32 + c] * y1[p * 32 + c];
+        for (int c = 0; c < SW; ++c)
+          acc += (double)d.w3[(size_t)n * K3 + c] * y0[p * SW + c] + (double)d.w3[(size_t)n * K3 + SW + c] * y1[p * SW + c];
         if (d.proj)
-          for (int c = 0; c < C; ++c) acc += (double)d.w3[(size_t)n * K3 + 64 + c] * xi[p * C + c];
+          for (int c = 0; c < C; ++c) acc += (double)d.w3[(size_t)n * K3 + 2 * SW + c] * xi[p * C + c];
         oi[p * CO + n] = (float)ht(acc);
       }
   }

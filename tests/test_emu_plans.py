@@ -76,9 +76,9 @@ def test_emulated_ragged_campplus_matches_per_utterance(arch):
 
 def test_step_bytes_priced_per_conv():
     """Per-step algorithmic bytes (the byte side of bench.py's per-launch roofline): every
-    conv step is priced; ERes2NetV2 layer2.1.conv3 (1x1, 104 -> 256 channels, residual) is
-    exactly input + weights + output + residual, fp32, and the fused stage-1 blocks
-    layer1.1.fused / layer1.0.fused are their input + output + the packed weight matrices."""
+    conv step is priced; ERes2NetV2 layer3.1.conv3 (1x1, 208 -> 512 channels, residual) is
+    exactly input + weights + output + residual, fp32, and the fused blocks layer1.1.fused /
+    layer1.0.fused / layer2.1.fused are their input + output + the packed weight matrices."""
     m = helpers.loaded_module('eres2netv2')
     em = EmuModel(m)
     B, T = 2, 40
@@ -89,8 +89,12 @@ def test_step_bytes_priced_per_conv():
         if kern.startswith(('conv_gemm', 'conv3x3', 'pw_gemm')):
             assert by > 0, name
     names = [name for name, _, _ in steps]
+    px3 = B * 20 * (T // 4)
+    assert nbytes[names.index("layer3.1.conv3")] == 4.0 * (px3 * 208 + 512 * 208 + px3 * 512 + px3 * 512)
+    # the stage-2 identity blocks are fused (res2block_s2.hip: 52-wide slices padded to 64)
     px2 = B * 40 * (T // 2)
-    assert nbytes[names.index("layer2.1.conv3")] == 4.0 * (px2 * 104 + 256 * 104 + px2 * 256 + px2 * 256)
+    w2 = 128 * 256 + 2 * 64 * 576 + 256 * 128
+    assert nbytes[names.index('layer2.1.fused')] == 8.0 * px2 * 256 + 4.0 * w2
     px = B * 80 * T
     w = 64 * 128 + 2 * 32 * 288 + 128 * 64
     assert nbytes[names.index('layer1.1.fused')] == 8.0 * px * 128 + 4.0 * w

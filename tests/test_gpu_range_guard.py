@@ -105,3 +105,29 @@ def test_two_streams_only_the_overflowing_forward_reruns():
     assert fa.value == 1 and fb.value == 0
     assert helpers.rel_err(oa.cpu().numpy(), ref_hot).max() < 1e-4
     assert helpers.rel_err(ob.cpu().numpy(), ref_clean).max() < 1e-4
+
+
+def test_large_weights_take_exact_gemm_layer():
+    """The tiled fp16x3 GEMM scales the weights' hi plane by 2^11 (one accumulator,
+    conv_gemm.hip), so a layer with a folded weight >= 31.5 runs on the exact-fp32 GEMM
+    instead (ConvDesc::wbig); the rest of the forward stays on fp16x3 and matches fp64."""
+    arch, key = 'eres2netv2', 'layer3.1.bn1.weight'
+    g = helpers.golden(arch)
+    m = _scaled(arch, key, 2000.0)   # Hardtanh(0, 20) keeps the activations bounded
+    feats = torch.from_numpy(g['feats2'][:3])
+    sd = {k: v.double() if v.is_floating_point() else v for k, v in m.state_dict().items()}
+    ref = models_ref.forward(arch, sd, feats.double()).numpy()
+    dev = torch.device('cuda', 0)
+    m = m.to(dev)
+    with torch.no_grad():
+        out = m(feats.to(dev)).cpu().numpy()
+    h = m._hip_handle(dev)
+    assert not h.last_forward_exact
+    kern = {name: k for name, k, _ in h.plan(*feats.shape[:2])}
+    assert kern['layer3.1.conv1'].startswith('conv_gemm_kernel<'), kern['layer3.1.conv1']
+    assert kern['layer3.2.conv1'].startswith('conv_gemm_x3_kernel<'), kern['layer3.2.conv1']
+    # the scaled BN makes the network ill-conditioned (the reference's own fp32 forward moves
+    # by ~1e-3): the bound is the north star's 1e-4 or twice the reference fp32 error
+    ref32 = models_ref.forward(arch, m.cpu().state_dict(), feats).numpy()
+    tol = max(1e-4, 2 * helpers.rel_err(ref32, ref).max())
+    assert helpers.rel_err(out, ref).max() < tol, (helpers.rel_err(out, ref).max(), tol)
