@@ -95,7 +95,8 @@ def roofline(model, feats, device, traffic_json):
         g['launches'] += 1
         g['steps'].append((fl, by, ms))
     kern, g = max(groups.items(), key=lambda kv: kv[1]['ms'])
-    x3 = '_x3_' in kern
+    # fp16x3 kernels: the tiled / persistent x3 GEMMs and the fused Res2Net blocks
+    x3 = '_x3_' in kern or kern.startswith('res2_block')
     peak = PEAK_X3_TFLOPS if x3 else PEAK_FP32_TFLOPS
 
     def attainable(steps, pk):
@@ -125,15 +126,27 @@ def roofline(model, feats, device, traffic_json):
             traffic = None if t is None else round(t['bytes_per_launch'])
         except Exception:
             traffic = None
+    # the kernel's binding roof: its launches' algorithmic bytes at 8 TB/s against their FLOPs
+    # at the MFMA peak; the larger floor names the bound and the unit `achieved` is quoted in
+    t_mfma = g['flops'] / (peak * 1e12)
+    t_hbm = g['bytes'] / (PEAK_HBM_GBS * 1e9)
+    hbm_bound = t_hbm > t_mfma
+    bytes_per_launch = g['bytes'] / g['launches']
+    gbs = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     return {
         'kernel': kern,
-        'bound': 'mfma',
-        'achieved': round(achieved, 3),
-        'peak': round(peak, 1),
-        'peak_basis': ('fp16 dense MFMA 2500 TFLOP/s / 3 (fp16x3 split products, fp32-accurate)' if x3
+        'bound': 'hbm' if hbm_bound else 'mfma',
+        'achieved': round(gbs, 1) if hbm_bound else round(achieved, 3),
+        'peak': PEAK_HBM_GBS if hbm_bound else round(peak, 1),
+        'peak_basis': ('HBM3E 8 TB/s' if hbm_bound else
+                       'fp16 dense MFMA 2500 TFLOP/s / 3 (fp16x3 split products, fp32-accurate)' if x3
                        else 'fp32 MFMA 157.3 TFLOP/s'),
-        'unit': 'TFLOP/s',
-        'frac': round(achieved / peak, 4),
+        'unit': 'GB/s' if hbm_bound else 'TFLOP/s',
+        'frac': round(gbs / PEAK_HBM_GBS, 4) if hbm_bound else round(achieved / peak, 4),
+        'mfma_side': {'achieved_TFLOPs': round(achieved, 3), 'peak_TFLOPs': round(peak, 1),
+                      'frac': round(achieved / peak, 4)},
+        'hbm_side': {'achieved_GBs': round(gbs, 1), 'peak_GBs': PEAK_HBM_GBS, 'frac': round(gbs / PEAK_HBM_GBS, 4),
+                     'algorithmic_bytes_per_launch': bytes_per_launch},
         'traffic': traffic,
         'traffic_unit': 'HBM bytes per launch (rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE, KiB -> B)',
         'launches_per_step': g['launches'],

@@ -19,7 +19,10 @@ from collections import defaultdict
 
 def short(name):
     m = re.search(r'([A-Za-z_0-9]+<[^()]*>)\s*\(', name)
-    return m.group(1) if m else name.split('(')[0].split('::')[-1]
+    if m:
+        return m.group(1)
+    name = name.replace('(anonymous namespace)::', '')
+    return name.split('(')[0].split('::')[-1]
 
 
 def main():
