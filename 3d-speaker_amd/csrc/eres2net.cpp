@@ -133,24 +133,27 @@ struct ERes2Builder {
     b.conv(p + ".local_att.3", e, a1, io2);
   }
 
-  // The whole block as one fused kernel (res2block.hip): ERes2NetV2 stage-1 shape (scale 2,
-  // slices <= 32 wide, 128 output channels) -- identity shortcut from 128 channels, or the
-  // stage's first block with a 1x1 stride-1 projection shortcut from 64 -- fp16x3 path,
-  // uniform lengths.
+  // The whole block as one fused kernel (res2block.hip / res2block_s2.hip), scale 2, fp16x3
+  // path, uniform lengths: stage 1 (slices <= 32 wide, 128 output channels) -- identity
+  // shortcut from 128 channels, or the stage's first block with a 1x1 stride-1 projection
+  // shortcut from 64; stage 2 (slices 33..64, 256 output channels) -- identity from 256, or
+  // the first block: 1x1 stride-2 conv1 and projection shortcut from 128.
   bool fusable(const std::string& p, const T4& x, int stride, int width, int Cout, bool use_aff) const {
     const bool sc = m.has(p + ".shortcut.0.weight");
-    const bool common = v2 && !use_aff && stride == 1 && scale == 2 && x.ld == x.C && !b.ragged && b.x3() &&
+    const bool common = v2 && !use_aff && scale == 2 && x.ld == x.C && !b.ragged && b.x3() &&
                         std::getenv("SPK_NO_BLOCK_FUSION") == nullptr;
     // stage 1 (res2block.hip): slices <= 32, 128 output channels, identity or 64 -> 128 projection
-    const bool s1 = width <= 32 && Cout == 128 &&
+    const bool s1 = stride == 1 && width <= 32 && Cout == 128 &&
                     (sc ? (x.C == 64 && std::getenv("SPK_NO_PROJ_FUSION") == nullptr) : x.C == 128);
-    // stage 2 (res2block_s2.hip): slices 33..64, 256 -> 256 identity
-    const bool s2 = width > 32 && width <= 64 && Cout == 256 && x.C == 256 && !sc &&
-                    std::getenv("SPK_NO_S2_FUSION") == nullptr;
+    // stage 2 (res2block_s2.hip): slices 33..64, 256 -> 256 identity, or 128 -> 256 at stride 2
+    // with the projection shortcut
+    const bool s2 = width > 32 && width <= 64 && Cout == 256 && std::getenv("SPK_NO_S2_FUSION") == nullptr &&
+                    (sc ? (x.C == 128 && stride == 2 && std::getenv("SPK_NO_PROJ_FUSION") == nullptr)
+                        : (x.C == 256 && stride == 1));
     return common && (s1 || s2);
   }
 
-  bool fused_block(const std::string& p, const T4& x, int width, int Cout, Buf outbuf, T4& out) {
+  bool fused_block(const std::string& p, const T4& x, int stride, int width, int Cout, Buf outbuf, T4& out) {
     const ChanMap xin = ChanMap::dense(x.C);
     const ChanMap om = ChanMap::dense(Cout);
     const int sw = width <= 32 ? 32 : 64;   // padded slice width of the fused kernel
@@ -165,13 +168,15 @@ struct ERes2Builder {
     const Packed& c3 = m.pack(p + ".conv3#fused", om, parts3, 2 * sw + (proj ? x.C : 0));
     // the stage-2 kernel's 3x3 convs use the one-accumulator fp16x3 form (hi_w scaled by 2^11)
     if (sw == 64 && (ca.wmax >= kX3WeightLimit || cb.wmax >= kX3WeightLimit)) return false;
-    const double px = (double)x.H * x.W;
+    const int Ho = (x.H - 1) / stride + 1, Wo = (x.W - 1) / stride + 1;
+    const double px = (double)Ho * Wo;   // output pixels (a strided block reads only those inputs)
     b.macs_per_utt += px * x.C * (double)width * 2 + 2.0 * px * 9.0 * width * width + px * (double)width * 2 * Cout +
                       (proj ? px * x.C * (double)Cout : 0.0);
-    out = T4{outbuf, Cout, x.H, x.W, Cout};
+    out = T4{outbuf, Cout, Ho, Wo, Cout};
     if (b.plan) {
       Res2Desc d;
-      d.nimg = b.B; d.H = x.H; d.W = x.W; d.C = x.C; d.width = width;
+      d.nimg = b.B; d.H = Ho; d.W = Wo; d.C = x.C; d.width = width;
+      d.stride = stride; d.Hin = x.H; d.Win = x.W;
       d.Cout = Cout; d.proj = proj;
       d.w1h = m.dhi(c1.w_off); d.w1l = m.dlo(c1.w_off); d.b1 = m.dptr(c1.b_off);
       d.wah = m.dhi(ca.w_off); d.wal = m.dlo(ca.w_off); d.ba = m.dptr(ca.b_off);
@@ -194,7 +199,7 @@ struct ERes2Builder {
     const int Ho = (x.H - 1) / stride + 1, Wo = (x.W - 1) / stride + 1;
     const int Cout = planes * expansion;
     T4 fo;
-    if (fusable(p, x, stride, width, Cout, use_aff) && fused_block(p, x, width, Cout, outbuf, fo)) return fo;
+    if (fusable(p, x, stride, width, Cout, use_aff) && fused_block(p, x, stride, width, Cout, outbuf, fo)) return fo;
     const ChanMap sl = ChanMap::slices(width, scale);
     const int wp = sl.n_phys / scale;
     const int ldt = sl.n_phys;

@@ -16,6 +16,8 @@ struct Res2Desc {
   float* out = nullptr;         // [nimg, H, W, Cout]
   int nimg = 0, H = 0, W = 0, C = 0;
   int Cout = 0;                 // output channels (0: C)
+  int stride = 1;               // conv1 / shortcut stride; H, W are the OUTPUT dims, the input is
+  int Hin = 0, Win = 0;         // [nimg, Hin, Win, C] (0: H, W); the stage-2 projection block uses 2
   bool proj = false;            // 1x1 projection shortcut + BN (ERes2NetV2.py:84-88), packed
                                 // into w3 as K columns 64 .. 64+C, its BN shift into b3
   int width = 0;                // Res2Net slice width (26 for ERes2NetV2 layer1, 52 for layer2), <= 64
@@ -29,7 +31,8 @@ struct Res2Desc {
 };
 
 bool res2_block_supported(const Res2Desc& d);
-// stage-2 identity blocks (256 -> 256, slices 33..64 wide): res2block_s2.hip
+// stage-2 blocks (slices 33..64 wide): the 256 -> 256 identity blocks and the stage's first
+// block (128 -> 256, stride 2, 1x1 projection shortcut): res2block_s2.hip
 bool res2_block_s2_supported(const Res2Desc& d);
 hipError_t launch_res2_block_s2(const Res2Desc& d, hipStream_t s);
 hipError_t launch_res2_block(const Res2Desc& d, hipStream_t s);

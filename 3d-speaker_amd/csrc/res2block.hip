@@ -481,13 +481,14 @@ int device_cus_r2() {
 bool res2_block_supported(const Res2Desc& d) {
   if (res2_block_s2_supported(d)) return true;
   const int co = d.Cout ? d.Cout : d.C;
-  const bool shape = d.proj ? (d.C == 64 && co == 128) : (d.C == 128 && co == 128);
+  const bool shape = d.stride == 1 && (!d.Hin || d.Hin == d.H) && (!d.Win || d.Win == d.W) &&
+                     (d.proj ? (d.C == 64 && co == 128) : (d.C == 128 && co == 128));
   return conv_use_x3() && shape && d.width >= 1 && d.width <= 32 && d.nimg > 0 && d.H > 0 && d.W > 0 &&
          d.w1h && d.w1l && d.wah && d.wal && d.wbh && d.wbl && d.w3h && d.w3l && d.b1 && d.ba && d.bb && d.b3;
 }
 
 std::string res2_block_kernel_name(const Res2Desc& d) {
-  if (res2_block_s2_supported(d)) return "res2_block_s2_kernel";
+  if (res2_block_s2_supported(d)) return d.proj ? "res2_block_s2_kernel<true>" : "res2_block_s2_kernel<false>";
   return d.proj ? "res2_block_kernel<64, 128, true>" : "res2_block_kernel<128, 128, false>";
 }
 

@@ -51,24 +51,31 @@ namespace {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+template <bool PROJ>
 struct S2 {
   static constexpr int NT = 512;
-  static constexpr int CI = 256, CO = 256, SW = 64;                 // channels; padded slice width
+  // channels: input (PROJ: the stage's first block, 128 -> 256 at stride 2), output, padded
+  // slice width
+  static constexpr int CI = PROJ ? 128 : 256, CO = 256, SW = 64, STR = PROJ ? 2 : 1;
   static constexpr int TH = 8, TW = 16;
   static constexpr int RH = TH + 4, RW = TW + 4, NR = RH * RW;      // S0 region 12 x 20 = 240 px
   static constexpr int PH = TH + 2, PW = TW + 2, NP = PH * PW;      // SP region 10 x 18 = 180 px
   static constexpr int NO = TH * TW;                                // 128 output px
   static constexpr int XCH = 16, NCH = NR / XCH;                    // 15 conv1 chunks of 16 px
-  static constexpr int XF = XCH * (CI / 4) / NT;                    // 2 float4 per thread per chunk
-  static constexpr int KS1 = CI / 32;                               // conv1 k-steps (8)
-  static constexpr int K3 = 2 * SW;                                 // conv3 K (CAT: 128)
-  static constexpr int KS3 = K3 / 32;                               // 4
+  static constexpr int XF = XCH * (CI / 4) / NT;                    // 2 (PROJ 1) float4 per thread per chunk
+  static constexpr int KS1 = CI / 32;                               // conv1 k-steps (8; PROJ 4)
+  static constexpr int KC = 2 * SW;                                 // CAT channels (128)
+  static constexpr int K3 = KC + (PROJ ? CI : 0);                   // conv3 K (CAT | PROJ: input tile)
+  static constexpr int KS3 = K3 / 32;                               // 4 (PROJ 8)
   static constexpr int KW = 9 * SW;                                 // 3x3 packed row length (576)
-  static constexpr int S0_PL = NR * SW, CAT_PL = NO * K3;           // plane sizes (halves)
+  static constexpr int S0_PL = NR * SW, CAT_PL = NO * KC;           // plane sizes (halves)
   static constexpr int R0_PL = S0_PL > CAT_PL ? S0_PL : CAT_PL;
   static constexpr int SP_PL = NP * SW, XC_PL = XCH * CI;
-  static constexpr int OFF_SP = 2 * R0_PL, OFF_XC = OFF_SP + 2 * SP_PL;
+  static constexpr int XN_PL = PROJ ? NO * CI : 0;                  // PROJ: the tile's input pixels
+  static constexpr int OFF_SP = 2 * R0_PL;
+  static constexpr int OFF_XC = OFF_SP + (2 * SP_PL > 2 * XN_PL ? 2 * SP_PL : 2 * XN_PL);
   static constexpr int LDS_HALVES = OFF_XC + 4 * XC_PL;
+  static constexpr int XNF = NO * (CI / 4) / NT;                    // PROJ: 8 float4 per thread
   static_assert(NR % XCH == 0 && XCH * (CI / 4) % NT == 0, "conv1 chunking");
   static_assert(2 * LDS_HALVES <= 160 * 1024, "LDS");
 };
@@ -79,9 +86,10 @@ __device__ __forceinline__ f32x4 mfma16(const f16x8& a, const f16x8& b, const f3
 }
 __device__ __forceinline__ f16x8 ld8(const uint16_t* p) { return *reinterpret_cast<const f16x8*>(p); }
 
+template <bool PROJ>
 __global__ void __launch_bounds__(512, 1)
 res2_block_s2_kernel(const Res2Desc d) {
-  using G = S2;
+  using G = S2<PROJ>;
   __shared__ __attribute__((aligned(16))) _Float16 lds[G::LDS_HALVES];
   _Float16* const S0h = lds;                  // S0 region, then (aliased) CAT
   _Float16* const S0l = lds + G::S0_PL;
@@ -89,15 +97,18 @@ res2_block_s2_kernel(const Res2Desc d) {
   _Float16* const CATl = lds + G::CAT_PL;
   _Float16* const SPh = lds + G::OFF_SP;
   _Float16* const SPl = SPh + G::SP_PL;
-  _Float16* const XCh = lds + G::OFF_XC;     // [buf][plane][px][256]
-  constexpr int CI = G::CI, SW = G::SW;
+  _Float16* const XCh = lds + G::OFF_XC;     // [buf][plane][px][CI]
+  _Float16* const XNh = lds + G::OFF_SP;      // PROJ: [plane][128 px][CI] over SP (free after convs.1)
+  constexpr int CI = G::CI, SW = G::SW, STR = G::STR;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // re-derived per tile from an opaque copy of the lane id (below): otherwise the compiler
   // hoists every lane-dependent address of all four phases out of the tile loop and keeps
   // them live (spilled) across it
   int l16 = lane & 15, lq = lane >> 4;
-  const int H = d.H, W = d.W;
+  const int H = d.H, W = d.W;                 // output dims
+  const int Hin = d.Hin ? d.Hin : H, Win = d.Win ? d.Win : W;
+  const size_t img_in = (size_t)Hin * Win * CI;
   const int ntx = (W + G::TW - 1) / G::TW, nty = (H + G::TH - 1) / G::TH;
   const int ntiles = d.nimg * ntx * nty;
 #if SPK_S2_PROF
@@ -127,7 +138,7 @@ res2_block_s2_kernel(const Res2Desc d) {
       const int px = ch * G::XCH + i / (CI / 4), q = i % (CI / 4);
       const int gy = min(max(ty0 - 2 + px / G::RW, 0), H - 1);
       const int gx = min(max(tx0 - 2 + px % G::RW, 0), W - 1);
-      v[j] = *reinterpret_cast<const f32x4*>(im + ((size_t)gy * W + gx) * CI + 4 * q);
+      v[j] = *reinterpret_cast<const f32x4*>(im + ((size_t)(STR * gy) * Win + STR * gx) * CI + 4 * q);
     }
   };
   auto store_chunk = [&](const f32x4 (&v)[G::XF], int buf) {
@@ -221,7 +232,7 @@ res2_block_s2_kernel(const Res2Desc d) {
   if (t_lo + slot < t_hi) {
     int im, ty0, tx0;
     tile_origin(t_lo + slot, im, ty0, tx0);
-    const float* p0 = d.x + (size_t)im * H * W * CI;
+    const float* p0 = d.x + (size_t)im * img_in;
     load_chunk(0, pf[0], ty0, tx0, p0);
     load_chunk(1, pf[1], ty0, tx0, p0);
     load_chunk(2, pf[2], ty0, tx0, p0);
@@ -238,10 +249,10 @@ res2_block_s2_kernel(const Res2Desc d) {
     wrow = (size_t)(16 * ntc + l16) * G::KW + 8 * lq;
     int img, y0, x0;
     tile_origin(t, img, y0, x0);
-    const float* const xim = d.x + (size_t)img * H * W * CI;
+    const float* const xim = d.x + (size_t)img * img_in;
     int nimg_, ny0, nx0;                      // the next tile (the last tile re-reads itself)
     tile_origin(t + nslot < t_hi ? t + nslot : t, nimg_, ny0, nx0);
-    const float* const nim = d.x + (size_t)nimg_ * H * W * CI;
+    const float* const nim = d.x + (size_t)nimg_ * img_in;
 
     // ================= 1. conv1 on the S0 region, one 16-pixel chunk per step: wave w
     //   computes its n-tile (channels 16w .. 16w+15 of the two slices) for the chunk; its A
@@ -355,7 +366,7 @@ res2_block_s2_kernel(const Res2Desc d) {
       const int r = p / G::PW - 1, c = p % G::PW - 1;
       if (r >= 0 && r < G::TH && c >= 0 && c < G::TW) {
         const int o = r * G::TW + c;
-        const int ao = o * G::K3 + 8 * (kbo ^ (o & 15)) + subo;
+        const int ao = o * G::KC + 8 * (kbo ^ (o & 15)) + subo;
         split_x3(y[i], h, l);
         *reinterpret_cast<h16x4*>(CATh + ao) = h;
         *reinterpret_cast<h16x4*>(CATl + ao) = l;
@@ -364,6 +375,17 @@ res2_block_s2_kernel(const Res2Desc d) {
     __syncthreads();
 
     S2_STAMP(5);
+    // PROJ: the tile's input pixels (conv3's second K operand, the strided 1x1 shortcut),
+    // requested now, in flight during convs.1, staged into LDS over SP after it
+    f32x4 xn[PROJ ? G::XNF : 1];
+    if constexpr (PROJ) {
+#pragma unroll
+      for (int j = 0; j < G::XNF; ++j) {
+        const int i = tid + G::NT * j, o = i / (CI / 4), q = i % (CI / 4);
+        const int gy = min(y0 + o / G::TW, H - 1), gx = min(x0 + o % G::TW, W - 1);
+        xn[j] = *reinterpret_cast<const f32x4*>(xim + ((size_t)(STR * gy) * Win + STR * gx) * CI + 4 * q);
+      }
+    }
     // ================= 3. convs.1 on the output tile (4 pixel tiles per wave)
     {
       int base[4];
@@ -382,7 +404,7 @@ res2_block_s2_kernel(const Res2Desc d) {
         for (int e = 0; e < 4; ++e) v[e] = htanh(z[i][e] + bbv[e]);
         h16x4 h, l;
         split_x3(v, h, l);
-        const int ao = o * G::K3 + 8 * ((8 + kbo) ^ (o & 15)) + subo;   // CAT channels 64..127
+        const int ao = o * G::KC + 8 * ((8 + kbo) ^ (o & 15)) + subo;   // CAT channels 64..127
         *reinterpret_cast<h16x4*>(CATh + ao) = h;
         *reinterpret_cast<h16x4*>(CATl + ao) = l;
       }
@@ -404,11 +426,27 @@ res2_block_s2_kernel(const Res2Desc d) {
       b3v[j] = *reinterpret_cast<const f32x4*>(d.b3 + n + 4 * lq);
     }
     __syncthreads();
+    if constexpr (PROJ) {                     // SP reads done: stage the input tile there
+#pragma unroll
+      for (int j = 0; j < G::XNF; ++j) {
+        const int i = tid + G::NT * j, o = i / (CI / 4), q = i % (CI / 4);
+        const int a = o * CI + 8 * ((q >> 1) ^ (o & 15)) + 4 * (q & 1);
+        h16x4 h, l;
+        split_x3(xn[j], h, l);
+        *reinterpret_cast<h16x4*>(XNh + a) = h;
+        *reinterpret_cast<h16x4*>(XNh + G::XN_PL + a) = l;
+      }
+      __syncthreads();
+    }
     S2_STAMP(7);
 
     // ================= 4. conv3 + bn3 + residual + Hardtanh -> out (8 pixel tiles, each with
     //   the wave's two n-tiles); the residual one pixel tile ahead
     auto res_load = [&](int pt, f32x4 (&r)[2]) {
+      if constexpr (PROJ) {                   // projection shortcut: in conv3's K, no residual
+        r[0] = r[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        return;
+      }
       const int gy = min(y0 + pt, H - 1), gx = min(x0 + l16, W - 1);
       const float* rp = xim + ((size_t)gy * W + gx) * CI + 4 * lq;
       r[0] = *reinterpret_cast<const f32x4*>(rp + 16 * wave);
@@ -429,9 +467,15 @@ res2_block_s2_kernel(const Res2Desc d) {
       f16x8 bh[G::KS3], bl[G::KS3];             // the pixel tile's whole K in flight at once
 #pragma unroll
       for (int ks = 0; ks < G::KS3; ++ks) {
-        const int a = o * G::K3 + 8 * ((4 * ks + lq) ^ (o & 15));
-        bh[ks] = *reinterpret_cast<const f16x8*>(CATh + a);
-        bl[ks] = *reinterpret_cast<const f16x8*>(CATl + a);
+        if (ks < 4) {
+          const int a = o * G::KC + 8 * ((4 * ks + lq) ^ (o & 15));
+          bh[ks] = *reinterpret_cast<const f16x8*>(CATh + a);
+          bl[ks] = *reinterpret_cast<const f16x8*>(CATl + a);
+        } else {
+          const int a = o * CI + 8 * ((4 * (ks - 4) + lq) ^ (o & 15));
+          bh[ks] = *reinterpret_cast<const f16x8*>(XNh + a);
+          bl[ks] = *reinterpret_cast<const f16x8*>(XNh + G::XN_PL + a);
+        }
       }
 #pragma unroll
       for (int ks = 0; ks < G::KS3; ++ks) {
@@ -476,7 +520,10 @@ int device_cus_s2() {
 
 bool res2_block_s2_supported(const Res2Desc& d) {
   const int co = d.Cout ? d.Cout : d.C;
-  return conv_use_x3() && !d.proj && d.C == 256 && co == 256 && d.width > 32 && d.width <= 64 && d.nimg > 0 &&
+  const int hin = d.Hin ? d.Hin : d.H, win = d.Win ? d.Win : d.W;
+  const bool shape = d.proj ? (d.C == 128 && d.stride == 2 && (hin - 1) / 2 + 1 == d.H && (win - 1) / 2 + 1 == d.W)
+                            : (d.C == 256 && d.stride == 1 && hin == d.H && win == d.W);
+  return conv_use_x3() && shape && co == 256 && d.width > 32 && d.width <= 64 && d.nimg > 0 &&
          d.H > 0 && d.W > 0 && d.w1h && d.w1l && d.wah && d.wal && d.wbh && d.wbl && d.w3h && d.w3l && d.b1 && d.ba &&
          d.bb && d.b3;
 }
@@ -486,7 +533,8 @@ hipError_t launch_res2_block_s2(const Res2Desc& d, hipStream_t s) {
   const int ntiles = d.nimg * ((d.W + 15) / 16) * ((d.H + 7) / 8);
   int grid = std::min(device_cus_s2(), (ntiles + 7) / 8 * 8);
   grid = std::max(8, grid / 8 * 8);
-  hipLaunchKernelGGL(res2_block_s2_kernel, dim3(grid), dim3(512), 0, s, d);
+  if (d.proj) hipLaunchKernelGGL(res2_block_s2_kernel<true>, dim3(grid), dim3(512), 0, s, d);
+  else hipLaunchKernelGGL(res2_block_s2_kernel<false>, dim3(grid), dim3(512), 0, s, d);
   return hipGetLastError();
 }
 

@@ -210,11 +210,15 @@ bool conv_use_x3() {
 // fused Res2Net block (res2block.hip, res2block_s2.hip), the kernels' contract in double
 // precision: conv1 + bn1 + Hardtanh -> s0 | s1 (slices padded to SW = 32 or 64 channels),
 // y0 = Ht(conv3x3(s0)), y1 = Ht(conv3x3(y0 + s1)), out = Ht(conv3(cat(y0, y1)) + x) -- or,
-// with the projection shortcut, Ht(conv3(cat(y0, y1, x))) -- zero padding at the edges
+// with the projection shortcut, Ht(conv3(cat(y0, y1, x))) -- zero padding at the edges; conv1
+// and the shortcut read input pixel (s y, s x) for output pixel (y, x) (stride s)
 bool res2_block_supported(const Res2Desc& d) {
   const int co = d.Cout ? d.Cout : d.C;
-  const bool s1 = (d.proj ? (d.C == 64 && co == 128) : (d.C == 128 && co == 128)) && d.width >= 1 && d.width <= 32;
-  const bool s2 = !d.proj && d.C == 256 && co == 256 && d.width > 32 && d.width <= 64;
+  const int hin = d.Hin ? d.Hin : d.H, win = d.Win ? d.Win : d.W;
+  const bool st1 = d.stride == 1 && hin == d.H && win == d.W;
+  const bool st2 = d.stride == 2 && (hin - 1) / 2 + 1 == d.H && (win - 1) / 2 + 1 == d.W;
+  const bool s1 = st1 && (d.proj ? (d.C == 64 && co == 128) : (d.C == 128 && co == 128)) && d.width >= 1 && d.width <= 32;
+  const bool s2 = (d.proj ? (st2 && d.C == 128) : (st1 && d.C == 256)) && co == 256 && d.width > 32 && d.width <= 64;
   return (s1 || s2) && d.w1 && d.wa && d.wb && d.w3 && d.b1 && d.ba && d.bb && d.b3;
 }
 std::string res2_block_kernel_name(const Res2Desc& d) { return "emu_res2_block<" + std::to_string(d.C) + ">"; }
@@ -223,6 +227,7 @@ hipError_t launch_res2_block(const Res2Desc& d, hipStream_t) {
   if (!res2_block_supported(d) || d.x == d.out) return hipErrorInvalidValue;
   const int SW = d.width <= 32 ? 32 : 64;
   const int H = d.H, W = d.W, C = d.C, CO = d.Cout ? d.Cout : d.C, K3 = d.proj ? 2 * SW + C : 2 * SW;
+  const int S = d.stride, Hin = d.Hin ? d.Hin : H, Win = d.Win ? d.Win : W;
   auto ht = [](double v) { return std::min(std::max(v, 0.0), 20.0); };
   std::vector<double> t1((size_t)H * W * 2 * SW), y0((size_t)H * W * SW), sp((size_t)H * W * SW), y1((size_t)H * W * SW);
   auto conv3 = [&](const std::vector<double>& in, const float* w, const float* b, std::vector<double>& out) {
@@ -240,12 +245,13 @@ hipError_t launch_res2_block(const Res2Desc& d, hipStream_t) {
         }
   };
   for (int img = 0; img < d.nimg; ++img) {
-    const float* xi = d.x + (size_t)img * H * W * C;
+    const float* xin = d.x + (size_t)img * Hin * Win * C;
     float* oi = d.out + (size_t)img * H * W * CO;
+    auto xi_at = [&](size_t p) { return xin + ((size_t)(p / W) * S * Win + (p % W) * S) * C; };
     for (size_t p = 0; p < (size_t)H * W; ++p)
       for (int n = 0; n < 2 * SW; ++n) {
         double acc = d.b1[n];
-        for (int k = 0; k < C; ++k) acc += (double)d.w1[(size_t)n * C + k] * xi[p * C + k];
+        for (int k = 0; k < C; ++k) acc += (double)d.w1[(size_t)n * C + k] * xi_at(p)[k];
         t1[p * 2 * SW + n] = ht(acc);
       }
     std::vector<double> s0((size_t)H * W * SW);
@@ -257,11 +263,11 @@ hipError_t launch_res2_block(const Res2Desc& d, hipStream_t) {
     conv3(sp, d.wb, d.bb, y1);
     for (size_t p = 0; p < (size_t)H * W; ++p)
       for (int n = 0; n < CO; ++n) {
-        double acc = d.b3[n] + (d.proj ? 0.0 : xi[p * C + n]);
+        double acc = d.b3[n] + (d.proj ? 0.0 : xi_at(p)[n]);
         for (int c = 0; c < SW; ++c)
           acc += (double)d.w3[(size_t)n * K3 + c] * y0[p * SW + c] + (double)d.w3[(size_t)n * K3 + SW + c] * y1[p * SW + c];
         if (d.proj)
-          for (int c = 0; c < C; ++c) acc += (double)d.w3[(size_t)n * K3 + 2 * SW + c] * xi[p * C + c];
+          for (int c = 0; c < C; ++c) acc += (double)d.w3[(size_t)n * K3 + 2 * SW + c] * xi_at(p)[c];
         oi[p * CO + n] = (float)ht(acc);
       }
   }

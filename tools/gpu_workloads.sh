@@ -10,6 +10,10 @@ for w in c1 c3 models; do
   rc=$?; cat gpurun_out/wl_$w.json; if [ $rc -ne 0 ]; then tail -5 gpurun_out/wl_$w.err; fi
   if fatal $rc; then exit $rc; fi
 done
+echo "== c3 fp16 mode $(date +%T)"
+timeout -k 10 300 python tools/bench_workloads.py c3 --precision fp16 > gpurun_out/wl_c3_fp16.json 2> gpurun_out/wl_c3_fp16.err
+rc=$?; cat gpurun_out/wl_c3_fp16.json; if [ $rc -ne 0 ]; then tail -5 gpurun_out/wl_c3_fp16.err; fi
+if fatal $rc; then exit $rc; fi
 echo "== c4 $(date +%T)"
 timeout -k 10 400 python tools/bench_c4.py ${C4_ARGS:-} > gpurun_out/wl_c4.json 2> gpurun_out/wl_c4.err
 rc=$?; cat gpurun_out/wl_c4.json; if [ $rc -ne 0 ]; then tail -5 gpurun_out/wl_c4.err; fi
