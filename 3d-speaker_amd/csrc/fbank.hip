@@ -73,6 +73,17 @@ __device__ __forceinline__ float prev_lane(float x, float first) {
   return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(first), __float_as_int(x), 0x138, 0xf, 0xf, false));
 }
 
+// log of a positive double, rounded to fp32: e = m 2^k with m in [1, 2) taken from the bits,
+// log e = k ln 2 (double) + logf(m) (fp32: |error| < 1e-7 absolute on [0, ln 2)).  The result
+// is stored as fp32, whose rounding (half an ulp, ~1e-6 at |log e| ~ 16) dominates; a double
+// log costs about ten times the instructions and was the largest share of the kernel
+__device__ __forceinline__ float log_d2f(double e) {
+  const int hi = __double2hiint(e), lo = __double2loint(e);
+  const int k = ((hi >> 20) & 0x7FF) - 1023;
+  const double m = __hiloint2double((hi & 0x000FFFFF) | 0x3FF00000, lo);
+  return (float)((double)k * 0.69314718055994530942 + (double)logf((float)m));
+}
+
 // LDS hand-off between lanes of one wave: order the memory ops, no cross-wave sync
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -289,7 +300,7 @@ fbank_frames_kernel(const float* __restrict__ wav, const int64_t* __restrict__ w
           for (int u = 0; u < 16; ++u)
             if (t + u < nbk) e += ps[min(b0 + t + u, 255)] * w[u];
         }
-        oa[f * n_mels + m] = (float)log(fmax(e, 1.1920928955078125e-07));
+        oa[f * n_mels + m] = log_d2f(fmax(e, 1.1920928955078125e-07));
       }
     }
     wave_sync();
