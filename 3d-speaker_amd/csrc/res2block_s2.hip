@@ -33,6 +33,9 @@
 #ifndef SPK_S2_PROF
 #define SPK_S2_PROF 0
 #endif
+#ifndef SPK_S2_RING
+#define SPK_S2_RING 3  // conv1 input chunks in flight in registers (a divisor of the 15 per tile)
+#endif
 #ifndef SPK_S2_EXP
 #define SPK_S2_EXP 0   // ablation builds only (tools/build_s2prof.sh)
 #endif
@@ -224,20 +227,22 @@ res2_block_s2_kernel(const Res2Desc d) {
   };
 
   // One continuous stream of conv1 input chunks over the block's tiles: chunk k of a tile sits
-  // in register-ring slot k % 3 (15 chunks per tile, so the next tile continues the pattern)
+  // in register-ring slot k % RG (RG divides the 15 chunks per tile, so the next tile continues
+  // the pattern; a 5-deep ring measured no faster than 3: the loads are not what conv1 waits on)
   // and is staged into LDS buffer xb ^ (k & 1), xb alternating per tile.  Invariant at the
-  // top of a tile: chunk 0 is in LDS buffer xb, chunks 1..3 are in flight in the ring.
-  f32x4 pf[3][G::XF];
+  // top of a tile: chunk 0 is in LDS buffer xb, chunks 1..RG are in flight in the ring.
+  constexpr int RG = SPK_S2_RING;
+  static_assert(G::NCH % RG == 0, "the ring must divide the chunks of a tile");
+  f32x4 pf[RG][G::XF];
   int xb = 0;
   if (t_lo + slot < t_hi) {
     int im, ty0, tx0;
     tile_origin(t_lo + slot, im, ty0, tx0);
     const float* p0 = d.x + (size_t)im * img_in;
-    load_chunk(0, pf[0], ty0, tx0, p0);
-    load_chunk(1, pf[1], ty0, tx0, p0);
-    load_chunk(2, pf[2], ty0, tx0, p0);
+#pragma unroll
+    for (int k = 0; k < RG; ++k) load_chunk(k, pf[k], ty0, tx0, p0);
     store_chunk(pf[0], 0);
-    load_chunk(3, pf[0], ty0, tx0, p0);
+    load_chunk(RG, pf[0], ty0, tx0, p0);
   }
   for (int t = t_lo + slot; t < t_hi; t += nslot) {
     {
@@ -265,20 +270,20 @@ res2_block_s2_kernel(const Res2Desc d) {
       a1l[ks] = ld8(d.w1l + o);
     }
 #pragma unroll 1
-    for (int c3 = 0; c3 < G::NCH; c3 += 3) {
+    for (int c3 = 0; c3 < G::NCH; c3 += RG) {
 #pragma unroll
-    for (int cj = 0; cj < 3; ++cj) {
+    for (int cj = 0; cj < RG; ++cj) {
       const int ch = c3 + cj;
       S2_STAMP(2);
       __syncthreads();
       S2_STAMP(0);
       // stage chunk ch + 1 (for ch = 14: the next tile's chunk 0), then request chunk ch + 4
       // (this tile's, or the next tile's ch - 11) into the slot it leaves
-      store_chunk(pf[(cj + 1) % 3], xb ^ ((ch + 1) & 1));
+      store_chunk(pf[(cj + 1) % RG], xb ^ ((ch + 1) & 1));
       {
-        const int cn = ch + 4;
+        const int cn = ch + 1 + RG;
         const bool nx = cn >= G::NCH;
-        load_chunk(nx ? cn - G::NCH : cn, pf[(cj + 1) % 3], nx ? ny0 : y0, nx ? nx0 : x0, nx ? nim : xim);
+        load_chunk(nx ? cn - G::NCH : cn, pf[(cj + 1) % RG], nx ? ny0 : y0, nx ? nx0 : x0, nx ? nim : xim);
       }
       S2_STAMP(1);
       const _Float16* xh = XCh + (xb ^ (ch & 1)) * 2 * G::XC_PL;

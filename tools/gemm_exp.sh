@@ -6,7 +6,7 @@
 set -eu
 cd "$(dirname "$0")/.."
 make -s -j8 -C 3d-speaker_amd/csrc
-objs=$(ls 3d-speaker_amd/build/*.o | grep -v conv_gemm)
+objs=$(ls 3d-speaker_amd/build/*.o | grep -v '/conv_gemm.o')
 for n in ${GEXPS:-1 2 3 5}; do
   (
     mkdir -p exp_libs/obj_g$n
