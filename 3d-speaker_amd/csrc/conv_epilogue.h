@@ -34,6 +34,19 @@ __device__ __forceinline__ void split_x3(const f32x4 v, h16x4& h, h16x4& l) {
   l = h16x4{l01[0], l01[1], l23[0], l23[1]};
 }
 
+// Output store of the fused blocks' conv3 (res2block*.hip).  SPK_NT_STORE=1 (experiment
+// builds): non-temporal, so the block's output does not displace its input halo from L2.
+#ifndef SPK_NT_STORE
+#define SPK_NT_STORE 0
+#endif
+__device__ __forceinline__ void block_store(f32x4* p, const f32x4& v) {
+#if SPK_NT_STORE
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();

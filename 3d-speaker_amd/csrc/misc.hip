@@ -13,55 +13,66 @@ namespace spk {
 
 namespace {
 
+// Tile of the stem: SF frequency rows x ST frames of one utterance per 256-thread block.  Thread
+// t owns channel quad q = t % (cout / 4) for every pixel it visits, so its 36 weights and 4
+// biases live in registers; the tile's (SF + 2) x (ST + 2) input window is staged in LDS once
+// (zero outside the image / past a ragged utterance's end).  Consecutive lanes store
+// consecutive 16-B quads of consecutive frames, i.e. every store instruction writes 1 KB of
+// contiguous output (channels-last rows): the kernel moves 4 * cout B per pixel out against
+// 4 B in, so the stores are what it is bound by.
+#ifndef SPK_STEM_SF
+#define SPK_STEM_SF 8   // frequency rows per block (2 / 4 / 8 measured 0.33 / 0.26 / 0.22 ms on ERes2NetV2)
+#endif
+constexpr int STEM_SF = SPK_STEM_SF, STEM_ST = 64;
+typedef float stem_f32x4 __attribute__((ext_vector_type(4)));
+
 __global__ void __launch_bounds__(256)
 stem_conv3x3_kernel(const float* __restrict__ feats, int B, int T, int F, const float* __restrict__ w,
                     const float* __restrict__ bias, int cout, int act, int wstride, float* __restrict__ out,
                     int ldo, const int* __restrict__ vlen, int* range_flag, const int* __restrict__ run_if) {
   SPK_GATE(run_if);
-  // thread -> (pixel, 16 output channels); pixel = (b, f, t) of the (F, T) image.  Weights and
-  // bias are staged in LDS once per block; 32-bit index math only.
-  __shared__ float ws[128 * 9];
-  __shared__ float bs[128];
-  for (int i = threadIdx.x; i < cout * 9; i += blockDim.x) ws[i] = w[(i / 9) * wstride + (i % 9)];
-  for (int i = threadIdx.x; i < cout; i += blockDim.x) bs[i] = bias[i];
+  constexpr int WF = STEM_SF + 2, WT = STEM_ST + 2;
+  __shared__ float win[WF * WT];
+  const int ntt = (T + STEM_ST - 1) / STEM_ST, nft = (F + STEM_SF - 1) / STEM_SF;
+  const int b = blockIdx.x / (nft * ntt), r = blockIdx.x % (nft * ntt);
+  const int f0 = (r / ntt) * STEM_SF, t0 = (r % ntt) * STEM_ST;
+  const int Tb = vlen ? vlen[b] : T;                 // ragged batches: frames past Tb are padding
+  for (int i = threadIdx.x; i < WF * WT; i += blockDim.x) {
+    const int ff = f0 - 1 + i % WF, tt = t0 - 1 + i / WF;   // f fastest: the rows are [t][F]
+    win[(i % WF) * WT + i / WF] = (ff >= 0 && ff < F && tt >= 0 && tt < Tb) ? feats[((size_t)b * T + tt) * F + ff] : 0.f;
+  }
+  const int nq = cout / 4, q = threadIdx.x % nq, ppp = blockDim.x / nq;   // pixels per pass
+  float wr[9][4], br[4];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wr[k][j] = w[(4 * q + j) * wstride + k];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) br[j] = bias[4 * q + j];
   __syncthreads();
-  const int groups = cout / 16;
-  const int total = B * F * T * groups;
   float amax = 0.f;                                  // range guard (common.h)
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
-    const int g = e % groups;
-    const int pix = e / groups;
-    const int t = pix % T;
-    const int bf = pix / T;
-    const int f = bf % F;
-    const int b = bf / F;
-    const int Tb = vlen ? vlen[b] : T;               // ragged batches: frames past Tb are padding
-    float in[9];
+  for (int p = threadIdx.x / nq; p < STEM_SF * STEM_ST; p += ppp) {
+    const int fl = p / STEM_ST, tl = p % STEM_ST;   // frame fastest: contiguous output rows
+    const int f = f0 + fl, t = t0 + tl;
+    if (f >= F || t >= T) continue;
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
       for (int dx = 0; dx < 3; ++dx) {
-        const int ff = f + dy - 1, tt = t + dx - 1;
-        in[dy * 3 + dx] = (ff >= 0 && ff < F && tt >= 0 && tt < Tb) ? feats[(b * T + tt) * F + ff] : 0.f;
+        const float x = win[(fl + dy) * WT + tl + dx];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = fmaf(x, wr[dy * 3 + dx][j], o[j]);
       }
-    const bool dead = t >= Tb;
-    float* op = out + (size_t)pix * ldo + g * 16;
+    stem_f32x4 v;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float4 o;
-      float* ov = &o.x;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = g * 16 + q * 4 + j;
-        float acc = 0.f;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) acc = fmaf(in[k], ws[c * 9 + k], acc);
-        acc += bs[c];
-        ov[j] = dead ? 0.f : (act == ACT_RELU ? fmaxf(acc, 0.f) : acc);
-        amax = fmaxf(amax, fabsf(ov[j]));
-      }
-      *reinterpret_cast<float4*>(op + q * 4) = o;
+    for (int j = 0; j < 4; ++j) {
+      float a = o[j] + br[j];
+      if (act == ACT_RELU) a = fmaxf(a, 0.f);
+      v[j] = t >= Tb ? 0.f : a;
+      amax = fmaxf(amax, fabsf(v[j]));
     }
+    *reinterpret_cast<stem_f32x4*>(out + (((size_t)b * F + f) * T + t) * ldo + 4 * q) = v;
   }
   range_note(range_flag, amax);
 }
@@ -108,11 +119,12 @@ tstp_kernel(const float* __restrict__ x, int B, int H, int W, int C, int ld, flo
 hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const float* w, const float* bias, int cout,
                                int act, int wstride, float* out, int ldo, hipStream_t s, const int* vlen,
                                int* range_flag) {
-  if (cout % 16 || cout > 128 || ldo % 4 || (long long)B * F * T * (cout / 16) >= (1LL << 31))
+  // cout / 4 channel quads must divide the 256 threads (one quad per thread for every pixel)
+  if (cout % 4 || cout > 128 || 256 % (cout / 4) || ldo % 4 || (long long)B * F * T * ldo >= (1LL << 40))
     return hipErrorInvalidValue;
-  const long long total = (long long)B * F * T * (cout / 16);
-  const int blocks = (int)std::min<long long>((total + 255) / 256, 65536);
-  hipLaunchKernelGGL(stem_conv3x3_kernel, dim3(blocks), dim3(256), 0, s, feats, B, T, F, w, bias, cout, act, wstride, out,
+  const long long blocks = (long long)B * ((F + STEM_SF - 1) / STEM_SF) * ((T + STEM_ST - 1) / STEM_ST);
+  if (blocks >= (1LL << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(stem_conv3x3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, feats, B, T, F, w, bias, cout, act, wstride, out,
                      ldo, vlen, range_flag, launch_gate());
   return hipGetLastError();
 }

@@ -455,7 +455,7 @@ res2_block_kernel(const Res2Desc d) {
             const float r = PROJ ? 0.f : (pt < 4 ? res_a[pt][e] : res_b[pt - 4][e]);
             v[e] = htanh(acc[e] + accx[e] * kLo + b3v[j][e] + r);
           }
-          *reinterpret_cast<f32x4*>(d.out + (((size_t)img * H + gy) * W + gx) * CO + n) = v;
+          block_store(reinterpret_cast<f32x4*>(d.out + (((size_t)img * H + gy) * W + gx) * CO + n), v);
         }
       }
     }

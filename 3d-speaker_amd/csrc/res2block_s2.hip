@@ -499,7 +499,7 @@ res2_block_s2_kernel(const Res2Desc d) {
           f32x4 v;
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = htanh(acc[j][e] + accx[j][e] * kLo + b3v[j][e] + res[pj][j][e]);
-          *reinterpret_cast<f32x4*>(d.out + (((size_t)img * H + gy) * W + gx) * G::CO + n) = v;
+          block_store(reinterpret_cast<f32x4*>(d.out + (((size_t)img * H + gy) * W + gx) * G::CO + n), v);
         }
       }
     }
