@@ -33,6 +33,9 @@
 #include "conv_epilogue.h"
 #include "res2block.h"
 
+#ifndef SPK_R2_RES_EARLY
+#define SPK_R2_RES_EARLY 1   // the second half of conv3's residual requested before convs.1 too
+#endif
 #ifndef SPK_R2_PROF
 #define SPK_R2_PROF 0
 #endif
@@ -343,6 +346,19 @@ res2_block_kernel(const Res2Desc d) {
       }
     }
 
+#if SPK_R2_RES_EARLY
+    // the second half as well: requested before the first MFMA of conv3 it would arrive an L2 /
+    // HBM round trip after conv3's first four pixel tiles (phase stamps: conv3 8.8k cycles per
+    // tile against 1.5k of MFMAs); the register ring is empty during convs.1, so the extra 16
+    // VGPRs are free there
+    f32x4 res_b[4];
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) {
+      const int gy = min(y0 + 4 + pt, H - 1), gx = min(x0 + l16, W - 1);
+      if constexpr (PROJ) res_b[pt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      else res_b[pt] = *reinterpret_cast<const f32x4*>(xim + ((size_t)gy * W + gx) * CI + 16 * wave + 4 * lq);
+    }
+#endif
     // ================= 3. convs.1 on the output tile (2 pixel tiles per wave)
     {
       f32x4 acc[2], accx[2];
@@ -403,6 +419,7 @@ res2_block_kernel(const Res2Desc d) {
     R2_STAMP(5);
 
     // ================= 4. conv3 + bn3 + residual + Hardtanh -> out (8 pixel tiles per wave)
+#if !SPK_R2_RES_EARLY
     // residual of the second half: requested before the first MFMA (the first half is in flight)
     f32x4 res_b[4];
 #pragma unroll
@@ -411,6 +428,7 @@ res2_block_kernel(const Res2Desc d) {
       if constexpr (PROJ) res_b[pt] = f32x4{0.f, 0.f, 0.f, 0.f};
       else res_b[pt] = *reinterpret_cast<const f32x4*>(xim + ((size_t)gy * W + gx) * CI + 16 * wave + 4 * lq);
     }
+#endif
     // the next tile's first three input chunks, behind the residual (vmcnt retires in order,
     // so the epilogue's wait for the residual does not wait for these)
     // unconditional (the last tile re-reads its own chunks): a load on only some paths

@@ -36,6 +36,9 @@
 #ifndef SPK_S2_RING
 #define SPK_S2_RING 3  // conv1 input chunks in flight in registers (a divisor of the 15 per tile)
 #endif
+#ifndef SPK_S2_RES_EARLY
+#define SPK_S2_RES_EARLY 0   // 1: conv3's whole residual requested before convs.1 (measured +1 %, off)
+#endif
 #ifndef SPK_S2_EXP
 #define SPK_S2_EXP 0   // ablation builds only (tools/build_s2prof.sh)
 #endif
@@ -391,6 +394,21 @@ res2_block_s2_kernel(const Res2Desc d) {
         xn[j] = *reinterpret_cast<const f32x4*>(xim + ((size_t)(STR * gy) * Win + STR * gx) * CI + 4 * q);
       }
     }
+#if SPK_S2_RES_EARLY
+    // conv3's residual (identity blocks), all eight pixel tiles, in flight during convs.1:
+    // requested one pixel tile ahead inside conv3 it arrived an L2 / HBM round trip late for
+    // every tile (phase stamps: conv3 15k cycles per tile against 6k of MFMAs)
+    f32x4 rese[PROJ ? 1 : 8][2];
+    if constexpr (!PROJ) {
+#pragma unroll
+      for (int pt = 0; pt < 8; ++pt) {
+        const int gy = min(y0 + pt, H - 1), gx = min(x0 + l16, W - 1);
+        const float* rp = xim + ((size_t)gy * W + gx) * CI + 4 * lq;
+        rese[pt][0] = *reinterpret_cast<const f32x4*>(rp + 16 * wave);
+        rese[pt][1] = *reinterpret_cast<const f32x4*>(rp + 16 * (wave + 8));
+      }
+    }
+#endif
     // ================= 3. convs.1 on the output tile (4 pixel tiles per wave)
     {
       int base[4];
@@ -457,6 +475,18 @@ res2_block_s2_kernel(const Res2Desc d) {
       r[0] = *reinterpret_cast<const f32x4*>(rp + 16 * wave);
       r[1] = *reinterpret_cast<const f32x4*>(rp + 16 * (wave + 8));
     };
+#if SPK_S2_RES_EARLY
+#pragma unroll
+    for (int pt = 0; pt < 8; ++pt) {
+      constexpr int pj = 0;
+      f32x4 res[1][2];
+      if constexpr (PROJ) {
+        res[0][0] = res[0][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        res[0][0] = rese[pt][0];
+        res[0][1] = rese[pt][1];
+      }
+#else
     f32x4 res[2][2];
     res_load(0, res[0]);
 #pragma unroll 1
@@ -465,6 +495,7 @@ res2_block_s2_kernel(const Res2Desc d) {
     for (int pj = 0; pj < 2; ++pj) {
       const int pt = p2 + pj;
       res_load(min(pt + 1, 7), res[pj ^ 1]);   // unconditional (the last re-reads itself)
+#endif
       const int o = 16 * pt + l16;
       f32x4 acc[2], accx[2];
 #pragma unroll
@@ -503,7 +534,9 @@ res2_block_s2_kernel(const Res2Desc d) {
         }
       }
     }
+#if !SPK_S2_RES_EARLY
     }
+#endif
     S2_STAMP(8);
     __syncthreads();                          // CAT reads done before the next tile's conv1
     S2_STAMP(9);
