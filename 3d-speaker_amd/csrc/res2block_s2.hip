@@ -39,6 +39,9 @@
 #ifndef SPK_S2_RES_EARLY
 #define SPK_S2_RES_EARLY 0   // 1: conv3's whole residual requested before convs.1 (measured +1 %, off)
 #endif
+#ifndef SPK_S2_WDIST
+#define SPK_S2_WDIST 1   // 3x3 weight fragments requested this many taps ahead (2 measured 8 % slower)
+#endif
 #ifndef SPK_S2_EXP
 #define SPK_S2_EXP 0   // ablation builds only (tools/build_s2prof.sh)
 #endif
@@ -178,7 +181,7 @@ res2_block_s2_kernel(const Res2Desc d) {
     // A fragments ping-pong between two register sets: a tap's MFMAs read one set while the
     // next tap's loads land in the other (no register copy, which would wait for the loads);
     // the scheduling barriers keep the compiler from sinking the loads next to their use
-    f16x8 wa[2][2][2];          // [set][hi / lo][kk]
+    f16x8 wa[SPK_S2_WDIST + 1][2][2];   // [set][hi / lo][kk]
     auto wload = [&](int tap, f16x8 (&w)[2][2]) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -216,6 +219,7 @@ res2_block_s2_kernel(const Res2Desc d) {
         for (int i = 0; i < NPT; ++i) acc[i] = mfma16(w[1][kk], bh[i], acc[i]);
       }
     };
+#if SPK_S2_WDIST == 1
     wload(0, wa[0]);
 #pragma unroll 1
     for (int tap = 0; tap < 8; tap += 2) {
@@ -225,6 +229,21 @@ res2_block_s2_kernel(const Res2Desc d) {
       taps(tap + 1, wa[1]);
     }
     taps(8, wa[0]);
+#else
+    // three register sets, two taps ahead (one tap of MFMAs is shorter than an L2 round
+    // trip); past the last tap the loads re-read tap 8 (unconditional: counted waits)
+    wload(0, wa[0]);
+    wload(1, wa[1]);
+#pragma unroll 1
+    for (int tap = 0; tap < 9; tap += 3) {
+      wload(tap + 2, wa[2]);
+      taps(tap, wa[0]);
+      wload(min(tap + 3, 8), wa[0]);
+      taps(tap + 1, wa[1]);
+      wload(min(tap + 4, 8), wa[1]);
+      taps(tap + 2, wa[2]);
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < NPT; ++i) acc[i] *= kLo;
   };
