@@ -70,6 +70,12 @@ struct ConvDesc {
   int wbig = 0;                 // a packed weight >= kX3WeightLimit: the tiled fp16x3 GEMM (whose
                                 // hi x hi product uses 2^11 hi_w) would overflow -> exact fp32 GEMM
   const int* run_if = nullptr;  // launch gate (below): set by launch_conv from launch_gate()
+  // K order of s0 in the packed weights and the A loaders.  0: k = tap * cin + c.  1 (deep
+  // multi-tap convs, cin a multiple of 32, no s1): 32-channel blocks outer, taps inner,
+  // k = ((c / 32) * taps + tap) * 32 + c % 32 -- a 32-deep K-tile is one tap of one channel
+  // block, and the taps of a block follow each other, so the block's input pixels are re-read
+  // from L2 within a few K-tiles instead of once per sweep over the whole K (runtime.cpp pack)
+  int kcb = 0;
 };
 
 // fp16x3 range guard.  The split-precision GEMMs represent an operand as two fp16 values,

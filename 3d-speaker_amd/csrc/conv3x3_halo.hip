@@ -644,7 +644,7 @@ bool halo_conv_supported(const ConvDesc& d) {
   const ConvSrc& s = d.s0;
   if (off == 1 || (off > 1 && off == s.cin)) return false;
   if (s.vlen) return false;   // masked (pre-activated) inputs take the implicit GEMM
-  return s.kh == 3 && s.kw == 3 && s.sh == 1 && s.sw == 1 && s.ph == 1 && s.pw == 1 && s.dh == 1 && s.dw == 1 &&
+  return !d.kcb && s.kh == 3 && s.kw == 3 && s.sh == 1 && s.sw == 1 && s.ph == 1 && s.pw == 1 && s.dh == 1 && s.dw == 1 &&
          !s.reflect && !s.pre_scale && !d.s1.p && d.s1.cin == 0 && d.ksplit == 1 && d.N <= 64 &&
          (s.cin == 28 || s.cin == 32 || s.cin == 52 || s.cin == 64) && d.Ho == s.H && d.Wo == s.W &&
          d.Kp >= 9 * s.cin && s.ld % 4 == 0 && (!s.p2 || s.ld2 % 4 == 0) &&

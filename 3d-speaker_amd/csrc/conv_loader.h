@@ -45,7 +45,13 @@ struct ALoader {
     }
     const int K0 = d.s0.kh * d.s0.kw * d.s0.cin;
     const int k = kt0 * BK + kq * 4;
-    if (k < K0) {
+    if (d.kcb) {   // channel-block-major K (common.h ConvDesc::kcb; BK == 32, checked on the host)
+      const int taps = d.s0.kh * d.s0.kw;
+      const int tap = kt0 % taps;
+      k_c = (kt0 / taps) * BK + kq * 4;
+      k_ky = k_c < d.s0.cin ? tap / d.s0.kw : d.s0.kh;
+      k_kx = tap % d.s0.kw;
+    } else if (k < K0) {
       const int tap = k / d.s0.cin;
       k_c = k - tap * d.s0.cin;
       k_ky = tap / d.s0.kw;
@@ -94,7 +100,15 @@ struct ALoader {
       }
       s.ok |= (ok0 || ok1) ? (1u << r) : 0u;
     }
-    if (in0) {
+    if (d.kcb) {   // next tap of the channel block; after its last tap the next block
+      if (in0) {
+        if (++k_kx == d.s0.kw) { k_kx = 0; ++k_ky; }
+        if (k_ky == d.s0.kh) {
+          k_c += BK;
+          if (k_c < d.s0.cin) k_ky = 0;
+        }
+      }
+    } else if (in0) {
       k_c += BK;
       while (k_c >= d.s0.cin && k_ky < d.s0.kh) {
         k_c -= d.s0.cin;
@@ -196,7 +210,10 @@ struct BufALoader {
     const int taps = d.s0.kh * d.s0.kw;
     const int K0 = taps * d.s0.cin;
     const int k = kt0 * BK + kq * 4;
-    if (k < K0) {
+    if (d.kcb) {   // channel-block-major K (common.h ConvDesc::kcb): t is the same in every lane
+      c = (kt0 / taps) * BK + kq * 4;
+      t = c < d.s0.cin ? kt0 % taps : taps;
+    } else if (k < K0) {
       t = k / d.s0.cin;
       c = k - t * d.s0.cin;
     } else {
@@ -230,6 +247,28 @@ struct BufALoader {
       if (PRE) ok |= (unsigned)b << r;
     }
     s.ok = ok;
+    advance(d);
+  }
+
+  // (tap, c) of the next K-tile
+  __device__ __forceinline__ void advance(const ConvDesc& d) {
+    const int taps = d.s0.kh * d.s0.kw;
+    if (d.kcb) {   // next tap of the channel block (uniform); after its last tap the next block
+      if (t < taps) {
+        ++t;
+        ++kx;
+        tdp += d.s0.dw;
+        if (kx == d.s0.kw) {
+          kx = 0;
+          tdp += d.s0.dh * d.s0.W - d.s0.kw * d.s0.dw;
+        }
+        if (t == taps) {
+          c += BK;
+          if (c < d.s0.cin) { t = 0; kx = 0; tdp = 0; }   // past the last block t stays at taps: zeros
+        }
+      }
+      return;
+    }
     c += BK;
     if (t < taps && c >= d.s0.cin) {   // cin >= BK: at most one tap boundary per K-tile
       c -= d.s0.cin;
@@ -247,21 +286,10 @@ struct BufALoader {
   // K-tile (BUF_OOB where the operand is padding / past M / past K), then advance (tap, c)
   __device__ __forceinline__ void offsets(const ConvDesc& d, uint32_t (&o)[AROWS]) {
     static_assert(!S1 && !ADD && !PRE, "plain operand only");
-    const int taps = d.s0.kh * d.s0.kw;
     const uint32_t toff = (uint32_t)(tdp * d.s0.ld + c) * 4u;
 #pragma unroll
     for (int r = 0; r < AROWS; ++r) o[r] = ((rmask[r] >> t) & 1u) ? roff[r] + toff : BUF_OOB;
-    c += BK;
-    if (t < taps && c >= d.s0.cin) {
-      c -= d.s0.cin;
-      ++t;
-      ++kx;
-      tdp += d.s0.dw;
-      if (kx == d.s0.kw) {
-        kx = 0;
-        tdp += d.s0.dh * d.s0.W - d.s0.kw * d.s0.dw;
-      }
-    }
+    advance(d);
   }
 
   __device__ __forceinline__ f32x4 value(const Slot& s, int r) const {

@@ -89,6 +89,7 @@ const Packed& Model::pack(const std::string& name, const ChanMap& out, const std
   std::vector<double> wd((size_t)N * Kp, 0.0), bd(N, 0.0);
   std::map<std::string, int> seen;
   bool has_bias = false;
+  int taps0 = 1, cinp0 = 0;
   for (const Part& part : parts) {
     const HostT& w = get(part.wkey);
     if (w.shape.size() < 2) throw SpkError(SPK_E_WEIGHTS, part.wkey + ": expected a conv/linear weight");
@@ -99,6 +100,8 @@ const Packed& Model::pack(const std::string& name, const ChanMap& out, const std
     const int nin = part.in.n_log(), cinp = part.in.n_phys;
     if (part.ci_lo + nin > cin) throw SpkError(SPK_E_WEIGHTS, part.wkey + ": in channels mismatch");
     if (part.kofs + taps * cinp > K) throw SpkError(SPK_E_INVALID, "internal: K overflow packing " + part.wkey);
+    taps0 = taps;
+    cinp0 = cinp;
     std::vector<double> s, t, si, ti;
     bn_fold(part.bn, cout, s, t);
     bn_fold(part.bn_in, cin, si, ti);
@@ -127,6 +130,22 @@ const Packed& Model::pack(const std::string& name, const ChanMap& out, const std
   }
   Packed p;
   p.N = N; p.K = K; p.Kp = Kp; p.has_bias = has_bias;
+  // channel-block-major K order for deep multi-tap convs (common.h ConvDesc::kcb)
+  static const bool kcb_on = [] {
+    const char* e = std::getenv("SPK_KCB");
+    return e && std::string(e) == "1";
+  }();
+  if (kcb_on && parts.size() == 1 && parts[0].kofs == 0 && taps0 > 1 && cinp0 >= 128 && cinp0 % 32 == 0 &&
+      K == taps0 * cinp0) {
+    std::vector<double> row(Kp);
+    for (int n = 0; n < N; ++n) {
+      double* wr = wd.data() + (size_t)n * Kp;
+      for (int tap = 0; tap < taps0; ++tap)
+        for (int c = 0; c < cinp0; ++c) row[((size_t)(c / 32) * taps0 + tap) * 32 + c % 32] = wr[(size_t)tap * cinp0 + c];
+      std::copy(row.begin(), row.begin() + K, wr);
+    }
+    p.kcb = 1;
+  }
   std::vector<float> wf(wd.begin(), wd.end()), bf(bd.begin(), bd.end());
   for (float v : wf) p.wmax = std::max(p.wmax, std::fabs(v));
   gemm_wmax = std::max(gemm_wmax, p.wmax);   // range guard (common.h)
@@ -172,6 +191,9 @@ void Builder::step(const std::string& name, Step s, const std::string& kernel, d
 void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const ConvIO& io, bool use_bias) {
   if (!plan) return;
   d.N = p.N; d.K = p.K; d.Kp = p.Kp;
+  d.kcb = p.kcb;
+  if (p.kcb && (d.s0.kh * d.s0.kw * d.s0.cin != d.K || d.s0.cin % 32 || io.s1))
+    throw SpkError(SPK_E_INVALID, "internal: channel-block K order on an unsupported conv: " + name);
   d.w = m.dptr(p.w_off);
   d.wh = exact ? nullptr : m.dhi(p.w_off);   // no split planes: the exact-fp32 kernels are chosen
   d.wl = exact ? nullptr : m.dlo(p.w_off);

@@ -89,6 +89,7 @@ struct Packed {
   size_t ps_off = SIZE_MAX, pt_off = SIZE_MAX;   // optional post-activation affine
   bool has_bias = false;
   float wmax = 0.f;                               // max |w| of the packed matrix
+  int kcb = 0;                                    // K order (common.h ConvDesc::kcb)
 };
 
 // One weight tensor's contribution to a packed GEMM.

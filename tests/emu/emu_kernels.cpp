@@ -67,7 +67,10 @@ hipError_t launch_conv(const ConvDesc& d, hipStream_t) {
     for (int k = 0; k < d.Kp; ++k) {
       float v = 0.f;
       if (k < K0) {
-        const int tap = k / d.s0.cin, c = k % d.s0.cin;
+        // K order (common.h ConvDesc::kcb): (tap, c) or 32-channel blocks outer, taps inner
+        const int taps = d.s0.kh * d.s0.kw;
+        const int tap = d.kcb ? (k / 32) % taps : k / d.s0.cin;
+        const int c = d.kcb ? (k / 32 / taps) * 32 + k % 32 : k % d.s0.cin;
         const int ky = tap / d.s0.kw, kx = tap % d.s0.kw;
         int hi = ho * d.s0.sh - d.s0.ph + ky * d.s0.dh;
         int wi = wo * d.s0.sw - d.s0.pw + kx * d.s0.dw;
