@@ -102,3 +102,18 @@ def test_step_bytes_priced_per_conv():
     w0 = 64 * 64 + 2 * 32 * 288 + 128 * 128
     assert nbytes[names.index('layer1.0.fused')] == 4.0 * px * (64 + 128) + 4.0 * w0
     assert not any(n.startswith('layer1.') and not n.endswith('.fused') for n in names)
+
+
+def test_emulated_plans_with_channel_block_k_order():
+    """ConvDesc::kcb (SPK_KCB=1, read once per process): the permuted weight packing and the
+    emulated loader order must still reproduce the oracle; a child process gets the flag."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, SPK_KCB='1')
+    r = subprocess.run([sys.executable, '-m', 'pytest', '-q', '-x', '-p', 'no:cacheprovider',
+                        os.path.join(here, 'test_emu_plans.py'), '-k',
+                        'test_emulated_plan_matches_oracle and (eres2netv2 or ecapa or resnet34)'],
+                       env=env, cwd=os.path.dirname(here), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
