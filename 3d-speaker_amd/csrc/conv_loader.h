@@ -282,7 +282,7 @@ struct BufALoader {
     }
   }
 
-  // LDS-DMA form (conv_gemm_dma.hip): this thread's byte offset of each row for the current
+  // LDS-DMA form (conv_gemm_ring.hip): this thread's byte offset of each row for the current
   // K-tile (BUF_OOB where the operand is padding / past M / past K), then advance (tap, c)
   __device__ __forceinline__ void offsets(const ConvDesc& d, uint32_t (&o)[AROWS]) {
     static_assert(!S1 && !ADD && !PRE, "plain operand only");

@@ -209,7 +209,7 @@ void build_ecapa(Builder& b, int T) {
         const Buf out = CATB.at((size_t)cat_off);
         b.step(p + ".se_apply", [=](const Ctx& c) {
           return launch_se_apply(c.resolve(H2), Ci, c.resolve(G), Ci, c.resolve(res), res_ld, c.resolve(out), catC, B, T,
-                                 Ci, c.stream);
+                                 Ci, c.stream, c.flag);
         });
       }
     }

@@ -1,4 +1,5 @@
 // libspk_hip C ABI + executor core (weight folding/packing, plans, workspace).
+#include <algorithm>
 #include "runtime.h"
 
 #include <cmath>
@@ -283,11 +284,13 @@ int hip_check(hipError_t e, const char* what) {
 
 }  // namespace
 
+bool spk::PlanPair::idle() const { return !last || hipEventQuery(last) == hipSuccess; }
+
 spk::PlanPair::~PlanPair() {
-  // an evicted pair is destroyed by the last forward holding it, after that forward has
-  // enqueued its graph: wait for the device before the executable graphs go
-  if (!graphs.empty()) (void)hipDeviceSynchronize();
+  // reached only for an idle pair (Model::retired sweep, handle destruction): no device-wide
+  // synchronisation here, which would stall every stream and break a caller's stream capture
   for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+  if (last) (void)hipEventDestroy(last);
 }
 
 namespace {
@@ -322,12 +325,19 @@ std::shared_ptr<PlanPair> get_pair(spk_model_t* h, int B, int T, bool ragged = f
   if (it != h->m.plans.end()) return it->second;
   if (ragged && h->m.cfg.arch != SPK_ARCH_CAMPPLUS && h->m.cfg.arch != SPK_ARCH_ECAPA)
     throw SpkError(SPK_E_UNSUPPORTED, "per-utterance lengths are implemented for CAM++ and ECAPA-TDNN only");
+  // drop retired pairs that no forward holds any more and whose last replay has completed
+  auto& rt = h->m.retired;
+  rt.erase(std::remove_if(rt.begin(), rt.end(),
+                          [](const std::shared_ptr<PlanPair>& p) { return p.use_count() == 1 && p->idle(); }),
+           rt.end());
   if (h->m.plans.size() >= Model::kMaxPlans) {
-    // evict the least recently used pair: forwards still holding it keep it alive
+    // evict the least recently used pair into the retired list: forwards still holding it,
+    // and replays of its graphs still on a stream, keep its graphs alive until they are done
     auto victim = h->m.plans.begin();
     for (auto p = h->m.plans.begin(); p != h->m.plans.end(); ++p)
       if (h->m.plan_use[p->first] < h->m.plan_use[victim->first]) victim = p;
     h->m.plan_use.erase(victim->first);
+    rt.push_back(victim->second);
     h->m.plans.erase(victim);
   }
   auto pair = std::make_shared<PlanPair>();
@@ -359,7 +369,7 @@ Plan* main_plan(const std::shared_ptr<PlanPair>& p) { return p->x3 ? p->x3.get()
 
 extern "C" {
 
-int spk_version(void) { return 1; }
+int spk_version(void) { return 2; }   // include/spk_hip.h: ABI revision
 
 const char* spk_last_error(void) { return g_last_error.c_str(); }
 
@@ -499,6 +509,12 @@ int spk_model_create(const spk_model_config_t* cfg, const spk_weight_t* weights,
 
 int spk_model_destroy(spk_model_t* model) {
   if (!model) return SPK_OK;
+  // the caller guarantees no forward of this handle is still being enqueued; replays already
+  // on a stream must finish before their executable graphs go
+  bool busy = false;
+  for (auto& kv : model->m.plans) busy = busy || !kv.second->idle();
+  for (auto& p : model->m.retired) busy = busy || !p->idle();
+  if (busy) (void)hipDeviceSynchronize();
   if (model->m.dweights) (void)hipFree(model->m.dweights);
   if (model->m.dsplit) (void)hipFree(model->m.dsplit);
   delete model;
@@ -619,7 +635,15 @@ static int run_graph(const char* fn, spk_model_t* model, PlanPair& pp, const flo
     }
   }
   if (int rc = hip_check(hipGraphLaunch(exec, stream), "hipGraphLaunch")) return rc;
-  return hip_check(hipMemcpyAsync(emb_out, out_s, pp.out_bytes, hipMemcpyDeviceToDevice, stream), "stage out");
+  if (int rc = hip_check(hipMemcpyAsync(emb_out, out_s, pp.out_bytes, hipMemcpyDeviceToDevice, stream), "stage out"))
+    return rc;
+  // completion marker of this replay (PlanPair::last): an evicted pair is freed only after it
+  {
+    std::lock_guard<std::mutex> lk(model->m.mu);
+    if (!pp.last)
+      if (int rc = hip_check(hipEventCreateWithFlags(&pp.last, hipEventDisableTiming), "hipEventCreate")) return rc;
+    return hip_check(hipEventRecord(pp.last, stream), "hipEventRecord");
+  }
 }
 
 static int run_forward(const char* fn, spk_model_t* model, const float* feats, int32_t B, int32_t T,

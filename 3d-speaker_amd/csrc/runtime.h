@@ -70,6 +70,11 @@ struct PlanPair {
   size_t stage_in = 0, stage_out = 0, stage_len = 0, stage_flag = 0;
   size_t in_bytes = 0, out_bytes = 0, len_bytes = 0;
   std::map<const void*, hipGraphExec_t> graphs;
+  // completion of the last graph replay enqueued from this pair (recorded on the caller's
+  // stream after the launch): an evicted pair's executable graphs are destroyed only once it
+  // has completed (Model::retired), never by synchronising the device
+  hipEvent_t last = nullptr;
+  bool idle() const;                // no replay of this pair can still be running
   ~PlanPair();
 };
 
@@ -120,6 +125,7 @@ struct Model {
   // a shared_ptr, so an evicted pair lives until its last forward has been enqueued
   std::map<std::tuple<int, int, int>, std::shared_ptr<PlanPair>> plans;
   std::map<std::tuple<int, int, int>, uint64_t> plan_use;
+  std::vector<std::shared_ptr<PlanPair>> retired;  // evicted pairs whose last replay may still run
   uint64_t plan_clock = 0;
   static constexpr size_t kMaxPlans = 24;
   bool force_exact = false;                       // a packed weight is out of fp16 range: exact path only

@@ -11,8 +11,10 @@ hipError_t launch_asp_stats(const float* x, int B, int T, int C, int ld, float e
                             const int* vlen = nullptr);
 hipError_t launch_attn_pool(const float* logit, int ldl, const float* x, int ldx, int B, int T, int C, float eps,
                             float* out, hipStream_t s, const int* vlen = nullptr);
+// range_flag (fp16x3 range guard, common.h): set when an output reaches kRangeLimit -- the SE
+// block outputs accumulate into the next blocks' inputs and the MFA conv's K-concatenated input
 hipError_t launch_se_apply(const float* x, int ldx, const float* gate, int ldg, const float* res, int ldr, float* out,
-                           int ldo, int B, int T, int C, hipStream_t s);
+                           int ldo, int B, int T, int C, hipStream_t s, int* range_flag = nullptr);
 // vlen (optional, ragged batches): valid frames per utterance
 hipError_t launch_cam_context(const float* x, int B, int T, int C, int ld, int seg, int nseg, float* out, int ldo,
                               hipStream_t s, const int* vlen = nullptr);

@@ -96,9 +96,10 @@ __global__ void attn_pool_kernel(const float* __restrict__ logit, int ldl, const
 
 __global__ void se_apply_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ gate, int ldg,
                                 const float* __restrict__ res, int ldr, float* __restrict__ out, int ldo, int B, int T,
-                                int C, const int* __restrict__ run_if) {
+                                int C, int* range_flag, const int* __restrict__ run_if) {
   SPK_GATE(run_if);
   const int C4 = C / 4;
+  float amax = 0.f;   // range guard (common.h): block outputs feed the next block's split GEMM
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * T * C4;
        e += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(e % C4) * 4;
@@ -109,8 +110,10 @@ __global__ void se_apply_kernel(const float* __restrict__ x, int ldx, const floa
     const float4 r = *reinterpret_cast<const float4*>(res + row * ldr + c);
     float4 o;
     o.x = v.x * g.x + r.x; o.y = v.y * g.y + r.y; o.z = v.z * g.z + r.z; o.w = v.w * g.w + r.w;
+    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
     *reinterpret_cast<float4*>(out + row * ldo + c) = o;
   }
+  range_note(range_flag, amax);
 }
 
 // ctx[b, s, c] = mean_T(x)[b, c] + mean over frames [100 s, min(100 s + 100, T)) of x[b, :, c]
@@ -301,10 +304,10 @@ hipError_t launch_attn_pool(const float* logit, int ldl, const float* x, int ldx
 }
 
 hipError_t launch_se_apply(const float* x, int ldx, const float* gate, int ldg, const float* res, int ldr, float* out,
-                           int ldo, int B, int T, int C, hipStream_t s) {
+                           int ldo, int B, int T, int C, hipStream_t s, int* range_flag) {
   if (C % 4 || ldx % 4 || ldg % 4 || ldr % 4 || ldo % 4) return hipErrorInvalidValue;
   hipLaunchKernelGGL(se_apply_kernel, dim3(grid_for((long long)B * T * C / 4)), dim3(256), 0, s, x, ldx, gate, ldg,
-                     res, ldr, out, ldo, B, T, C, launch_gate());
+                     res, ldr, out, ldo, B, T, C, range_flag, launch_gate());
   return hipGetLastError();
 }
 

@@ -362,9 +362,13 @@ def run(args):
             exchange_fn(emb, world, rank, B * world)
         return emb
 
+    handle = model._hip_handle(device)
+    reruns, checked = 0, 0                    # fp16x3 range guard: forwards the exact plan re-ran
     with torch.no_grad():
         for _ in range(args.warmup):
             step()
+            reruns += int(handle.last_forward_exact)   # untimed: checked after every warm-up forward
+            checked += 1
         torch.cuda.synchronize()
         if dist:
             tdist.barrier()
@@ -378,6 +382,8 @@ def run(args):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         assert torch.isfinite(emb).all(), 'non-finite embeddings'
+        reruns += int(handle.last_forward_exact)       # the last timed forward (same input every step)
+        checked += 1
         if dist:
             t = torch.tensor([dt], device=device)
             tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
@@ -431,6 +437,8 @@ def run(args):
             'model_tflops_achieved': round(value * flops / 1e12, 3),
             'model_gflop_per_utt': round(flops / 1e9, 3),
             'exchange': exchange,
+            # the range guard's exact-fp32 re-run must never fire on this input
+            'exact_reruns': {'count': reruns, 'forwards_checked': checked},
             'roofline': roof,
             'cpu_baseline': cpu,
         }

@@ -93,6 +93,7 @@ typedef struct {
   int32_t reserved[6];
 } spk_model_config_t;
 
+/* ABI revision: 2 (spk_model_range_check's seven-argument form, spk_model_config_t.pooling) */
 int spk_version(void);
 const char* spk_last_error(void);
 

@@ -335,6 +335,8 @@ hipError_t hipGetDevice(int* d) { *d = 0; return hipSuccess; }
 hipError_t hipGetLastError(void) { return hipSuccess; }
 const char* hipGetErrorString(hipError_t e) { return e == hipSuccess ? "hipSuccess" : "emulated hip error"; }
 hipError_t hipEventCreate(hipEvent_t* e) { *e = nullptr; return hipSuccess; }
+hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) { *e = nullptr; return hipSuccess; }
+hipError_t hipEventQuery(hipEvent_t) { return hipSuccess; }
 hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }
 hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
 hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
@@ -397,13 +399,14 @@ hipError_t launch_attn_pool(const float* l, int ldl, const float* x, int ldx, in
   return hipSuccess;
 }
 hipError_t launch_se_apply(const float* x, int ldx, const float* g, int ldg, const float* r, int ldr, float* out,
-                           int ldo, int B, int T, int C, hipStream_t) {
+                           int ldo, int B, int T, int C, hipStream_t, int* range_flag) {
   EMU_GATE();
   for (int b = 0; b < B; ++b)
     for (int t = 0; t < T; ++t)
       for (int c = 0; c < C; ++c) {
         const size_t row = (size_t)b * T + t;
         out[row * ldo + c] = x[row * ldx + c] * g[(size_t)b * ldg + c] + r[row * ldr + c];
+        emu_range_note(range_flag, out[row * ldo + c]);
       }
   return hipSuccess;
 }

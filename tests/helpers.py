@@ -73,3 +73,12 @@ def rel_err(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
     return np.linalg.norm(a - b, axis=-1) / np.linalg.norm(b, axis=-1)
+
+
+def took_exact_rerun(module, device=None):
+    """True when the module's last HIP forward was recomputed by the exact-fp32 plan (the
+    fp16x3 range guard): on the golden inputs every model stays in fp16 range,
+    so a re-run there means a kernel wrote an out-of-range value (synchronises the stream)."""
+    import torch
+    dev = device or torch.device('cuda', torch.cuda.current_device())
+    return module._hip_handle(dev).last_forward_exact

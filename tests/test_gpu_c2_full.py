@@ -28,7 +28,9 @@ def test_c2_full_batch_rows_vs_oracle():
         feats = _hip.fbank(x, 80, mean_nor=True)
         assert feats.shape == (B, 198, 80)
         emb = m(feats).cpu().numpy()
+        assert not helpers.took_exact_rerun(m)   # the split plan ran: no range-guard re-run
         tail = m(feats[B - 8:].contiguous()).cpu().numpy()
+        assert not helpers.took_exact_rerun(m)
     assert np.isfinite(emb).all()
     # tail rows of the 2 GB batch == the same utterances in a batch of 8
     assert helpers.rel_err(emb[B - 8:], tail).max() < 5e-5

@@ -29,6 +29,8 @@ def test_golden_embeddings(arch):
     for i in range(3):
         with torch.no_grad():
             emb = m(torch.from_numpy(g[f'feats{i}']).cuda()).cpu().numpy()
+        # the fp16x3 plan produced these embeddings, not the range guard's exact re-run
+        assert not helpers.took_exact_rerun(m), (arch, i)
         assert emb.shape == g[f'emb32_{i}'].shape
         e64 = helpers.rel_err(emb, g[f'emb64_{i}']).max()
         e32 = helpers.rel_err(emb, g[f'emb32_{i}']).max()

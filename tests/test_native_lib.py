@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     for s in declared_symbols():
         assert hasattr(lib, s), s
         assert s in _hip.SYMBOLS, f'{s} not bound in speakerlab/_hip.py'
-    assert lib.spk_version() >= 1
+    assert lib.spk_version() == 2   # INTEGRATION.md 'ABI conventions'
 
 
 def test_library_is_gfx950_code_object():
