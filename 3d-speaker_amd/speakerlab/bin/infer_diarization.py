@@ -46,6 +46,9 @@ parser.add_argument('--include_overlap', action='store_true', help='Include over
 parser.add_argument('--hf_access_token', type=str, help='hf_access_token for pyannote/segmentation-3.0 model')
 parser.add_argument('--diable_progress_bar', action='store_true', help='Close the progress bar')
 parser.add_argument('--nprocs', default=None, type=int, help='Num of procs')
+parser.add_argument('--shard_chunks', action='store_true',
+                    help='MI355X build: shard every file\'s chunks across the --nprocs ranks (one process '
+                         'group, one all-gather of the embeddings) instead of one file per process')
 parser.add_argument('--speaker_num', default=None, type=int, help='Oracle num of speaker')
 parser.add_argument('--no_chunk_after_vad', action='store_true', help='One embedding per VAD segment')
 parser.add_argument('--vad_min_speech_ms', default=200.0, type=float)
@@ -166,7 +169,7 @@ class Diarization3Dspeaker:
                  model_cache_dir=None, no_chunk_after_vad=False, vad_min_speech_ms=None, vad_max_silence_ms=None,
                  vad_energy_threshold=None, vad_boundary_expansion_ms=None, vad_boundary_energy_percentile=None,
                  vad_threshold=0.5, cluster_mer_cos=0.3, cluster_fix_cos_thr=0.3, cluster_min_cluster_size=0,
-                 chunk_dur=1.5, chunk_step=0.75, batch_size=64, synthetic_weights=False, vad='auto'):
+                 chunk_dur=1.5, chunk_step=0.75, batch_size=64, synthetic_weights=False, vad='auto', group=None):
         if include_overlap and hf_access_token is None:
             raise ValueError('hf_access_token is required when include_overlap is True.')
         if include_overlap:
@@ -185,6 +188,11 @@ class Diarization3Dspeaker:
         self.fs = self.feature_extractor.sample_rate
         self.speaker_num = speaker_num
         self.no_chunk_after_vad = no_chunk_after_vad
+        # one file's chunks sharded across the ranks of a torch.distributed group (SURVEY §8(e),
+        # C5): whole embedding batches per rank, ONE all-gather of the embeddings, a row block
+        # of the cosine affinity per rank gathered for the clustering (every rank clusters the
+        # same matrix; rank 0 writes).  None: one process does everything (the reference).
+        self.group = group
         self.output_field_labels = None
         self.last_vad_time = self.last_vad_time_raw = self.last_vad_time_processed = None
         self.last_vad_masked_audio = self.last_vad_refined_mask = self.last_vad_processed_mask = None
@@ -232,29 +240,70 @@ class Diarization3Dspeaker:
     def chunk(self, st, ed):
         return vad_post.chunk(st, ed, self.chunk_dur, self.chunk_step)
 
+    def _dist(self):
+        if self.group is None:
+            return 0, 1
+        import torch.distributed as dist
+        return dist.get_rank(self.group), dist.get_world_size(self.group)
+
+    def embed_batches(self, dev_wav, starts, lens, max_len, lo, hi):
+        """Embeddings of chunks [lo, hi) in batches of ``batchsize`` starting at ``lo``, each
+        chunk circle-padded to ``max_len`` samples (reference :621-639), on the device."""
+        ar = torch.arange(max_len, device=self.device)
+        out = []
+        with torch.no_grad():
+            for b in range(lo, hi, self.batchsize):
+                e = min(hi, b + self.batchsize)
+                s, n = starts[b:e, None], lens[b:e, None]
+                idx = s + torch.remainder(ar[None], n)
+                feats = self.feature_extractor.batch(dev_wav[idx])
+                out.append(self.embedding_model(feats))
+        if not out:
+            return torch.empty((0, self.embedding_dim()), dtype=torch.float32, device=self.device)
+        return torch.cat(out)
+
+    def embedding_dim(self):
+        return int(getattr(self.embedding_model, 'embedding_size', 192))
+
     def do_emb_extraction(self, chunks, wav):
-        """Sub-segments circle-padded to the longest one (reference :621-639), on the device."""
+        """Sub-segments circle-padded to the longest one (reference :621-639), on the device.
+        With a process group, each rank embeds a contiguous block of whole batches and one
+        all-gather (RCCL over xGMI with nccl) gives every rank all N embeddings."""
         x = wav[0] if wav.dim() == 2 else wav
         L = x.shape[0]
         starts = torch.tensor([min(int(st * self.fs), L) for st, _ in chunks], dtype=torch.int64)
         lens = torch.tensor([min(int(ed * self.fs), L) for _, ed in chunks], dtype=torch.int64) - starts
         if int(lens.min()) <= 0:
             raise ValueError('empty sub-segment')
-        max_len = int(lens.max())
+        max_len = int(lens.max())                   # over ALL chunks: the same padding on every rank
         dev_wav = x.to(self.device, torch.float32)
         starts, lens = starts.to(self.device), lens.to(self.device)
-        ar = torch.arange(max_len, device=self.device)
-        out = []
-        with torch.no_grad():
-            for b in range(0, len(chunks), self.batchsize):
-                s, n = starts[b:b + self.batchsize, None], lens[b:b + self.batchsize, None]
-                idx = s + torch.remainder(ar[None], n)
-                feats = self.feature_extractor.batch(dev_wav[idx])
-                out.append(self.embedding_model(feats))
-        return torch.cat(out).cpu().numpy()
+        rank, world = self._dist()
+        n = len(chunks)
+        if world == 1:
+            return self.embed_batches(dev_wav, starts, lens, max_len, 0, n).cpu().numpy()
+        from speakerlab.utils.distributed import all_gather_rows, batch_shard
+        bounds = [batch_shard(n, self.batchsize, r, world) for r in range(world)]
+        lo, hi = bounds[rank]
+        local = self.embed_batches(dev_wav, starts, lens, max_len, lo, hi)
+        return all_gather_rows(local, [e - s for s, e in bounds], self.group).cpu().numpy()
 
     def do_clustering(self, chunks, embeddings, speaker_num=None):
-        labels = self.cluster(embeddings, speaker_num=speaker_num if speaker_num is not None else self.speaker_num)
+        spk = speaker_num if speaker_num is not None else self.speaker_num
+        rank, world = self._dist()
+        if world == 1 or len(embeddings) <= 1:
+            labels = self.cluster(embeddings, speaker_num=spk)
+        else:
+            # each rank's row block of the N x N cosine affinity (MFMA kernel), gathered
+            from speakerlab.utils.distributed import all_gather_rows, shard_bounds
+            from speakerlab import _hip
+            n = len(embeddings)
+            X = torch.from_numpy(np.ascontiguousarray(embeddings, dtype=np.float32)).to(self.device)
+            bounds = [shard_bounds(n, r, world) for r in range(world)]
+            s, e = bounds[rank]
+            block = _hip.cosine_affinity(X[s:e], X)
+            S = all_gather_rows(block, [b - a for a, b in bounds], self.group)
+            labels = self.cluster.from_affinity(embeddings, S, speaker_num=spk)
         speaker_num = labels.max() + 1
         segs = [[c[0], c[1], int(j)] for c, j in zip(chunks, labels)]
         return speaker_num, vad_post.compressed_seg(segs)
@@ -355,16 +404,25 @@ def write_side_files(diar, wav_path, out_file, wav_id, elapsed, plot=True):
         json.dump({'pairs': pairs}, f, indent=2)
 
 
-def main_process(rank, nprocs, args, wav_list):
+def main_process(rank, nprocs, args, wav_list, port=None):
     device = torch.device('cuda', rank % torch.cuda.device_count())
     torch.cuda.set_device(device)
+    group = None
+    if args.shard_chunks and nprocs > 1:
+        import torch.distributed as dist
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ['MASTER_PORT'] = str(port)
+        dist.init_process_group('nccl', rank=rank, world_size=nprocs, device_id=device)
+        group = dist.group.WORLD
     diar = Diarization3Dspeaker(
         device, args.include_overlap, args.hf_access_token, args.speaker_num, args.model_cache_dir,
         args.no_chunk_after_vad, args.vad_min_speech_ms, args.vad_max_silence_ms, args.vad_energy_threshold,
         args.vad_boundary_expansion_ms, args.vad_boundary_energy_percentile, args.vad_threshold,
         args.cluster_mer_cos, args.cluster_fix_cos_thr, args.cluster_min_cluster_size, args.chunk_dur,
-        args.chunk_step, args.batch_size, synthetic_weights=args.synthetic_weights, vad=args.vad)
-    mine = wav_list[rank::nprocs]               # one file per process, as the reference (:924)
+        args.chunk_step, args.batch_size, synthetic_weights=args.synthetic_weights, vad=args.vad, group=group)
+    # one file per process, as the reference (:924); with --shard_chunks every rank takes part
+    # in every file and rank 0 writes the outputs
+    mine = wav_list if group is not None else wav_list[rank::nprocs]
     if rank == 0 and not args.diable_progress_bar:
         from tqdm import tqdm
         mine = tqdm(mine, desc='Rank 0 processing')
@@ -372,13 +430,21 @@ def main_process(rank, nprocs, args, wav_list):
         t0 = time.time()
         diar(wav_path)
         elapsed = time.time() - t0
+        if group is not None and rank != 0:
+            continue
         wav_id = os.path.basename(wav_path).rsplit('.', 1)[0]
         if args.out_dir is not None:
             out_file = os.path.join(args.out_dir, f'{wav_id}.{args.out_type}')
         else:
             out_file = f'{wav_path.rsplit(".", 1)[0]}.{args.out_type}'
         diar.save_diar_output(out_file, wav_id)
+        diar.group = None                         # the side files' pair pass is rank 0's alone
         write_side_files(diar, wav_path, out_file, wav_id, elapsed)
+        diar.group = group
+    if group is not None:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main(argv=None):
@@ -397,15 +463,19 @@ def main(argv=None):
     ngpus = torch.cuda.device_count()
     if ngpus == 0:
         raise RuntimeError('[ERROR]: no ROCm device: the MI355X build has no CPU inference path')
-    nprocs = min(len(wav_list), args.nprocs or ngpus)
+    nprocs = (args.nprocs or ngpus) if args.shard_chunks else min(len(wav_list), args.nprocs or ngpus)
     print(f'[INFO]: Set {nprocs} processes to extract embeddings.')
     if args.out_dir is not None:
         os.makedirs(args.out_dir, exist_ok=True)
     if nprocs == 1:
         main_process(0, 1, args, wav_list)
     else:
+        import socket
         import torch.multiprocessing as mp
-        mp.spawn(main_process, nprocs=nprocs, args=(nprocs, args, wav_list))
+        with socket.socket() as so:
+            so.bind(('127.0.0.1', 0))
+            port = so.getsockname()[1]
+        mp.spawn(main_process, nprocs=nprocs, args=(nprocs, args, wav_list, port))
 
 
 if __name__ == '__main__':

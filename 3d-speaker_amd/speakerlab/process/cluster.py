@@ -113,13 +113,22 @@ def spectral_labels_gpu(X, min_num_spks=1, max_num_spks=10, pval=0.02, min_pnum=
     symmetrisation + Laplacian (csrc/spectral.hip), all eigenpairs by rocSOLVER ssyevd (in
     place of ARPACK eigsh 'SM'); eigen-gap and k-means on the host as in the reference."""
     import torch
-    from sklearn.cluster._kmeans import k_means
     from speakerlab import _hip
     if not torch.cuda.is_available():
         raise _hip.HipError('spectral clustering runs on the ROCm device; none is available')
     t = torch.as_tensor(np.ascontiguousarray(X, dtype=np.float32)).cuda()
-    n = t.shape[0]
-    S = _hip.cosine_affinity(t)
+    return spectral_labels_gpu_affinity(_hip.cosine_affinity(t), min_num_spks, max_num_spks, pval, min_pnum,
+                                        oracle_num)
+
+
+def spectral_labels_gpu_affinity(S, min_num_spks=1, max_num_spks=10, pval=0.02, min_pnum=6, oracle_num=None):
+    """spectral_labels_gpu from a cosine affinity already on the device (e.g. row blocks
+    gathered from several GPUs, ``bin/infer_diarization.py --shard_chunks``)."""
+    import torch
+    from sklearn.cluster._kmeans import k_means
+    from speakerlab import _hip
+    S = torch.as_tensor(S).to('cuda', torch.float32).contiguous()
+    n = S.shape[0]
     L = _hip.spectral_laplacian(S, pruned_count(n, pval, min_pnum))
     del S
     kk = min(max_num_spks + 1, n)
@@ -146,6 +155,13 @@ class SpectralCluster:
         oracle = kwargs.get('speaker_num', None)
         return spectral_labels_gpu(X, self.min_num_spks, self.max_num_spks, self.pval if pval is None else pval,
                                    self.min_pnum, self.k if oracle is None else oracle)
+
+    def from_affinity(self, S, **kwargs):
+        pval = kwargs.get('pval', None)
+        oracle = kwargs.get('speaker_num', None)
+        return spectral_labels_gpu_affinity(S, self.min_num_spks, self.max_num_spks,
+                                            self.pval if pval is None else pval, self.min_pnum,
+                                            self.k if oracle is None else oracle)
 
 
 class UmapHdbscan:
@@ -177,6 +193,9 @@ class AHCluster:
     def __call__(self, X, **kwargs):
         return ahc_labels(cosine_affinity(X), self.fix_cos_thr)
 
+    def from_affinity(self, S, **kwargs):
+        return ahc_labels(S.cpu().numpy() if hasattr(S, 'cpu') else np.asarray(S), self.fix_cos_thr)
+
 
 class CommonClustering:
     """Dispatch (N < cluster_line -> AHC), then minor-cluster filtering and centroid merging."""
@@ -203,6 +222,24 @@ class CommonClustering:
             labels = self.cluster_for_short(X)
         else:
             labels = self.cluster(X, **kwargs)
+        return self._finish(labels, X)
+
+    def from_affinity(self, X, S, **kwargs):
+        """__call__ with the N x N cosine affinity of X given (e.g. assembled from the row
+        blocks several GPUs computed): the same dispatch, clustering and post-processing."""
+        assert len(X.shape) == 2 and S.shape[0] == S.shape[1] == X.shape[0]
+        if X.shape[0] <= 1:
+            return np.zeros(X.shape[0], dtype=int)
+        if X.shape[0] < self.cluster_line or not hasattr(self.cluster, 'from_affinity'):
+            if X.shape[0] >= self.cluster_line:   # a back-end without an affinity form (umap_hdbscan)
+                labels = self.cluster(X, **kwargs)
+            else:
+                labels = self.cluster_for_short.from_affinity(S)
+        else:
+            labels = self.cluster.from_affinity(S, **kwargs)
+        return self._finish(labels, X)
+
+    def _finish(self, labels, X):
         labels = self.filter_minor_cluster(labels, X, self.min_cluster_size)
         if self.mer_cos is not None:
             labels = self.merge_by_cos(labels, X, self.mer_cos)

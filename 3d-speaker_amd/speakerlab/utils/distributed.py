@@ -46,6 +46,37 @@ def all_gather_embeddings(local: torch.Tensor, n_total: int, group=None) -> torc
     return torch.cat(rows, 0)
 
 
+def all_gather_rows(local: torch.Tensor, counts, group=None) -> torch.Tensor:
+    """Concatenate every rank's [counts[r], ...] block in rank order on every rank (blocks of
+    unequal size are padded to max(counts) for the collective).  nccl gathers device tensors
+    with one ``all_gather_into_tensor``; gloo gathers host copies."""
+    world = dist.get_world_size(group)
+    assert len(counts) == world and local.shape[0] == counts[dist.get_rank(group)]
+    per = max(max(counts), 1)
+    nccl = dist.get_backend(group) == 'nccl'
+    src = local if nccl else local.cpu()
+    padded = torch.zeros((per,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+    padded[:src.shape[0]] = src
+    if nccl:
+        out = torch.empty((world * per,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+        dist.all_gather_into_tensor(out, padded, group=group)
+        blocks = out.view((world, per) + tuple(src.shape[1:]))
+    else:
+        parts = [torch.empty_like(padded) for _ in range(world)]
+        dist.all_gather(parts, padded, group=group)
+        blocks = torch.stack(parts)
+    return torch.cat([blocks[r, :counts[r]] for r in range(world)], 0).to(local.device)
+
+
+def batch_shard(n: int, batch: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous block [start, stop) of WHOLE batches of ``batch`` items for ``rank``: every
+    rank runs exactly the batches a single process would run (same batch composition, hence
+    bitwise the same per-row results as one process)."""
+    nb = math.ceil(n / batch) if batch > 0 else 0
+    b0, b1 = shard_bounds(nb, rank, world)
+    return min(n, b0 * batch), min(n, b1 * batch)
+
+
 def affinity_row_block(emb_all: torch.Tensor, rank: int, world: int, out: Optional[torch.Tensor] = None):
     """(row0, [rows, N]) cosine affinity of this rank's rows against all N embeddings,
     computed on the GPU by ``spk_cosine_affinity``."""
