@@ -26,12 +26,19 @@
 // Numerics are those of conv_gemm.hip's fp16x3 kernels, with two accumulators (hi x hi, and
 // the cross terms at 2^11):  x * w ~= hi_x hi_w + 2^-11 (hi_x lo_w + lo_x hi_w), products exact,
 // fp32 sums.
+#include <algorithm>
 #include <cstdlib>
 #include <string>
 
 #include "common.h"
 #include "conv_epilogue.h"
 #include "conv_loader.h"
+
+#ifndef SPK_REXP
+#define SPK_REXP 0   // ablation builds only (tools/ring_exp.sh): 1 no MFMA, 2 no in-loop DMA,
+                     // 3 no epilogue stores, 4 no split, 5 = 1 + 2 + 3, 6 empty kernel of the
+                     // same resources; 0 = the product kernel
+#endif
 
 namespace spk {
 
@@ -83,16 +90,42 @@ conv_gemm_ring_kernel(const ConvDesc d) {
   SPK_GATE(d.run_if);
   __shared__ __attribute__((aligned(16))) float lds[RNS * RSTAGE / 4];   // the only LDS object
   char* const lb = reinterpret_cast<char*>(lds);
+#if SPK_REXP == 6
+  if (d.N > 0) {   // launch-cost probe: same resources, no work
+    if (threadIdx.x == 1000) lds[0] = 0.f;
+    return;
+  }
+#endif
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int M = d.nimg * d.Ho * d.Wo;
   const int nN = (d.N + RBN - 1) / RBN;
   const int nM = (M + RBM - 1) / RBM;
-  const int lid = xcd_remap(blockIdx.x, nM * nN);   // the N tiles of one M tile share an XCD (its A in L2)
-  const int mt = lid / nN, nt = lid % nN;
-  const int m0 = mt * RBM, n0 = nt * RBN;
+  const int ntile = nM * nN;
   const int nkt = d.Kp / RBK;
+
+  // ---- tiles of this block.  One tile per block when the grid covers them (XCD remap: the N
+  // tiles of one M tile on one XCD, their A in its L2); otherwise persistent: the tiles are
+  // split into 8 contiguous ranges, one per XCD (blocks b and b + 8 share an XCD), and the
+  // XCD's blocks take its range round-robin, so the blocks running together on an XCD work
+  // on neighbouring tiles (same M tile, consecutive N tiles) and sweep M together.
+  const int G = gridDim.x;
+  int tbase, tstep, ntb;
+  if (G >= ntile) {
+    tbase = xcd_remap(blockIdx.x, ntile);
+    tstep = 1;
+    ntb = blockIdx.x < ntile ? 1 : 0;
+  } else {
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3, nper = G >> 3;   // G % 8 == 0 (host)
+    const int q = ntile >> 3, r = ntile & 7;
+    const int cnt = q + (x < r ? 1 : 0);
+    tbase = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
+    tstep = nper;
+    ntb = j < cnt ? (cnt - j + nper - 1) / nper : 0;
+  }
+  if (ntb == 0) return;
+  const int total = ntb * nkt;
 
   // ---- A DMA: instruction j of wave w fills pixel rows 64 j + 8 w .. +7 (8 rows x 128 B);
   // lane p -> row 64 j + 8 w + (p >> 3), LDS slot p & 7, i.e. source k-quad
@@ -100,7 +133,6 @@ conv_gemm_ring_kernel(const ConvDesc d) {
   const int aq = (lane & 7) ^ ((4 * wave + (lane >> 4)) & 7);
   using AL = BufALoader<4, 64, RBK, false, false, false>;
   AL al;
-  al.init(d, m0, 8 * wave + (lane >> 3), aq, 0);
   const int a_dst = (8 * wave) * 128;          // + 64 rows (8 KB) per instruction j
   // ---- B DMA: instruction i = 2 w + j (j = 0, 1) fills plane i >> 3 (hi / lo), channels
   // 16 (i & 7) .. +15; lane p -> channel 16 (i & 7) + (p >> 2), slot p & 3, source chunk
@@ -109,24 +141,37 @@ conv_gemm_ring_kernel(const ConvDesc d) {
   const __amdgpu_buffer_rsrc_t brs = make_rsrc(plane ? d.wl : d.wh);
   const int cq = (lane & 3) ^ ((lane >> 4) & 3);
   uint32_t boff[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = n0 + 16 * ((2 * wave + j) & 7) + (lane >> 2);
-    boff[j] = n < d.N ? ((uint32_t)n * d.Kp + cq * 8) * 2u : BUF_OOB;
-  }
   const int b_dst = RA_STAGE + plane * RB_PLANE + ((2 * wave) & 7) * 1024;   // + 1 KB per j
 
-  auto issue = [&](int kt, int stage) {
+  // issue cursor (tile ii of this block, K-tile ik): runs two K-tiles ahead of the compute
+  // cursor, across tile boundaries, so a tile's first K-tiles land during the previous
+  // tile's last K-tiles and epilogue
+  int ii = 0, ik = 0;
+  auto set_issue_tile = [&](int i) {
+    const int lid = tbase + i * tstep;
+    const int m0 = (lid / nN) * RBM, n0 = (lid % nN) * RBN;
+    al.init(d, m0, 8 * wave + (lane >> 3), aq, 0);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + 16 * ((2 * wave + j) & 7) + (lane >> 2);
+      boff[j] = n < d.N ? ((uint32_t)n * d.Kp + cq * 8) * 2u : BUF_OOB;
+    }
+  };
+  auto issue_next = [&](int stage) {
     uint32_t ao[4];
     al.offsets(d, ao);
     char* const sb = lb + stage * RSTAGE;
-    const int koff = __builtin_amdgcn_readfirstlane(kt * RBK * 2);   // K-tile byte offset in a weight row
+    const int koff = __builtin_amdgcn_readfirstlane(ik * RBK * 2);   // K-tile byte offset in a weight row
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(al.r0, (lds_ptr_t)(sb + a_dst + j * 8192), 16, (int)ao[j], 0, 0, 0);
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, (lds_ptr_t)(sb + b_dst + j * 1024), 16, (int)boff[j], koff, 0, 0);
+    if (++ik == nkt) {
+      ik = 0;
+      if (++ii < ntb) set_issue_tile(ii);
+    }
   };
 
   // two accumulators per tile: hi_x hi_w, and the 2^11-scaled cross terms hi_x lo_w + lo_x hi_w
@@ -159,9 +204,18 @@ conv_gemm_ring_kernel(const ConvDesc d) {
         wl[j] = *reinterpret_cast<const f16x8*>(bp + RB_PLANE);
       }
       f16x8 xh, xl;
+#if SPK_REXP == 4
+      xh = __builtin_bit_cast(f16x8, a0);
+      xl = __builtin_bit_cast(f16x8, a1);
+#else
       split8(a0, a1, xh, xl);
+#endif
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
+#if SPK_REXP == 1 || SPK_REXP >= 5
+        acc[j][0] += (float)wh[j][0] * (float)xh[0] + (float)wl[j][1] * (float)xl[1];
+        continue;
+#endif
         acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh[j], xh, acc[j], 0, 0, 0);
         accx[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl[j], xh, accx[j], 0, 0, 0);
         accx[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh[j], xl, accx[j], 0, 0, 0);
@@ -169,83 +223,101 @@ conv_gemm_ring_kernel(const ConvDesc d) {
     }
   };
 
-  // prologue: K-tiles 0 and 1 in flight (clamped: past the last tile a stage is refilled with
-  // it again, unread, so every iteration waits for the same count)
-  issue(0, 0);
-  issue(min(1, nkt - 1), 1);
-  int st = 0;
-  for (int kt = 0; kt < nkt; ++kt) {
-    // this wave's DMA of K-tile kt has landed (the RDMA of kt+1 stay in flight); every wave's
-    // fragment reads of the stage the next issue overwrites (read at kt-1) are done
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RDMA) : "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    issue(min(kt + 2, nkt - 1), st == 0 ? 2 : st - 1);
-    compute(st);
-    st = st == 2 ? 0 : st + 1;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
   // ---- fused epilogue from the accumulators: lane (li, lh) holds pixel m of the wave, and in
   // register quad g of tile j the channels n = n0 + 32 j + 8 g + 4 lh .. +3 (MFMA D layout:
   // row = (r & 3) + 8 (r >> 2) + 4 lh, column = li)
-  const int m = m0 + arow;
-  const bool mok = m < M;
-  const int mm = mok ? m : 0;
-  const bool rowz = mok && row_masked(d, m);
   float amax = 0.f;
-  const int img = mm / (d.Ho * d.Wo), wo = mm % d.Wo;
-  // one 32-channel tile at a time: its residual / AFF operand loads are all issued before use
+  auto epilogue = [&](int lid) {
+    const int m0 = (lid / nN) * RBM, n0 = (lid % nN) * RBN;
+    const int m = m0 + arow;
+    const bool mok = m < M;
+    const int mm = mok ? m : 0;
+    const bool rowz = mok && row_masked(d, m);
+    const int img = mm / (d.Ho * d.Wo), wo = mm % d.Wo;
+    // one 32-channel tile at a time: its residual / AFF operand loads are all issued before use
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    f32x4 ra[4], xa[4], ya[4];
+    for (int j = 0; j < 4; ++j) {
+      f32x4 ra[4], xa[4], ya[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int n = n0 + 32 * j + 8 * g + 4 * lh;
-      const int nn = n < d.N ? n : 0;
-      ra[g] = xa[g] = ya[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (d.res) ra[g] = *reinterpret_cast<const f32x4*>(d.res + (size_t)mm * d.ldr + nn);
-      if (d.affx) {
-        xa[g] = *reinterpret_cast<const f32x4*>(d.affx + (size_t)mm * d.ldx + nn);
-        ya[g] = *reinterpret_cast<const f32x4*>(d.affy + (size_t)mm * d.ldy + nn);
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + 32 * j + 8 * g + 4 * lh;
+        const int nn = n < d.N ? n : 0;
+        ra[g] = xa[g] = ya[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (d.res) ra[g] = *reinterpret_cast<const f32x4*>(d.res + (size_t)mm * d.ldr + nn);
+        if (d.affx) {
+          xa[g] = *reinterpret_cast<const f32x4*>(d.affx + (size_t)mm * d.ldx + nn);
+          ya[g] = *reinterpret_cast<const f32x4*>(d.affy + (size_t)mm * d.ldy + nn);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + 32 * j + 8 * g + 4 * lh;
+        if (!mok || n >= d.N) continue;
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = fmaf(accx[j][4 * g + e], 1.0f / 2048.0f, acc[j][4 * g + e]);
+        if (d.bias) o += *reinterpret_cast<const f32x4*>(d.bias + n);
+        if (d.rowbias) o += *reinterpret_cast<const f32x4*>(d.rowbias + (size_t)img * d.rowbias_ld + n);
+        o += ra[g];
+        if (d.affx) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float t = 1.0f + tanhf(o[e]);
+            o[e] = xa[g][e] * t + ya[g][e] * (2.0f - t);
+          }
+        } else {
+          f32x4 ps = {1.f, 1.f, 1.f, 1.f}, pt = {0.f, 0.f, 0.f, 0.f};
+          if (d.post_scale) {
+            ps = *reinterpret_cast<const f32x4*>(d.post_scale + n);
+            pt = *reinterpret_cast<const f32x4*>(d.post_shift + n);
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float x = apply_act(o[e], d.act);
+            if (d.post_scale) x = x * ps[e] + pt[e];
+            o[e] = apply_act(x, d.act2);
+          }
+          if (d.gate)
+            o *= *reinterpret_cast<const f32x4*>(d.gate + ((size_t)img * d.gate_nseg + wo / d.gate_seg) * d.gate_ld + n);
+        }
+        if (rowz) o = f32x4{0.f, 0.f, 0.f, 0.f};
+        amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+#if SPK_REXP == 3 || SPK_REXP >= 5
+        if (o[0] == 1234.5f)
+#endif
+        *reinterpret_cast<f32x4*>(out_at(d, m, n)) = o;
       }
     }
+  };
+
+  // prologue: the first two K-tiles of the block in flight
+  set_issue_tile(0);
+  issue_next(0);
+  if (total > 1) issue_next(1);
+  int st = 0, ci = 0, ck = 0;
+  for (int it = 0; it < total; ++it) {
+    // this wave's DMA of iteration `it` has landed (the RDMA of it+1 stay in flight); every
+    // wave's fragment reads of the stage the next issue overwrites (read at it-1) are done
+    if (it + 1 < total) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RDMA) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#if SPK_REXP != 2 && SPK_REXP < 5
+    if (it + 2 < total) issue_next(st == 0 ? 2 : st - 1);
+#endif
+    compute(st);
+    st = st == 2 ? 0 : st + 1;
+    if (++ck == nkt) {
+      epilogue(tbase + ci * tstep);
+      ck = 0;
+      ++ci;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int n = n0 + 32 * j + 8 * g + 4 * lh;
-      if (!mok || n >= d.N) continue;
-      f32x4 o;
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = fmaf(accx[j][4 * g + e], 1.0f / 2048.0f, acc[j][4 * g + e]);
-      if (d.bias) o += *reinterpret_cast<const f32x4*>(d.bias + n);
-      if (d.rowbias) o += *reinterpret_cast<const f32x4*>(d.rowbias + (size_t)img * d.rowbias_ld + n);
-      o += ra[g];
-      if (d.affx) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float t = 1.0f + tanhf(o[e]);
-          o[e] = xa[g][e] * t + ya[g][e] * (2.0f - t);
-        }
-      } else {
-        f32x4 ps = {1.f, 1.f, 1.f, 1.f}, pt = {0.f, 0.f, 0.f, 0.f};
-        if (d.post_scale) {
-          ps = *reinterpret_cast<const f32x4*>(d.post_scale + n);
-          pt = *reinterpret_cast<const f32x4*>(d.post_shift + n);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float x = apply_act(o[e], d.act);
-          if (d.post_scale) x = x * ps[e] + pt[e];
-          o[e] = apply_act(x, d.act2);
-        }
-        if (d.gate)
-          o *= *reinterpret_cast<const f32x4*>(d.gate + ((size_t)img * d.gate_nseg + wo / d.gate_seg) * d.gate_ld + n);
-      }
-      if (rowz) o = f32x4{0.f, 0.f, 0.f, 0.f};
-      amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
-      *reinterpret_cast<f32x4*>(out_at(d, m, n)) = o;
+        for (int r = 0; r < 16; ++r) acc[j][r] = accx[j][r] = 0.f;
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   range_note(d.range_flag, amax);
 }
 
@@ -277,9 +349,22 @@ int ring_tile_blocks(const ConvDesc& d) {
   return ((M + RBM - 1) / RBM) * ((d.N + RBN - 1) / RBN);
 }
 
+// persistent grid: one block per CU (SPK_RING_GRID overrides; 0 = one block per tile)
+static int ring_grid(int tiles) {
+  static const int g = [] {
+    const char* e = std::getenv("SPK_RING_GRID");
+    if (e) return std::atoi(e);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return cus;
+  }();
+  if (g <= 0 || tiles <= g) return tiles;
+  return std::max(8, g / 8 * 8);   // the tile split assumes whole groups of 8 (XCDs)
+}
+
 hipError_t launch_ring(const ConvDesc& d, hipStream_t s) {
   if (!ring_supported(d)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(conv_gemm_ring_kernel, dim3(ring_tile_blocks(d)), dim3(RNT), 0, s, d);
+  hipLaunchKernelGGL(conv_gemm_ring_kernel, dim3(ring_grid(ring_tile_blocks(d))), dim3(RNT), 0, s, d);
   return hipGetLastError();
 }
 

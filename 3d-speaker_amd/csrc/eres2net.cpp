@@ -65,6 +65,53 @@ struct ERes2Builder {
 
   double pix(const T4& t) const { return (double)t.H * t.W; }
 
+  // ASTP (pooling_layers.py:93-104, global_context_att=False) of x [B, F, T, C] into stats
+  // [B, 2*F*C] ((f, c) order, as TSTP): linear1 over the reference's (C*F) channels is a conv
+  // whose kernel spans the F frequency rows (weight [bottleneck, C*F] read as [bottleneck][C][F]
+  // -- the same memory -- so tap f, channel c is reference channel c*F + f), + tanh; linear2
+  // writes its C*F logits in (f, c) order; one pass then pools every (f, c) over time.
+  void astp(const T4& x, const Buf& stats) {
+    const int B = b.B, F = x.H, T = x.W, C = x.C;
+    const std::string w1 = "pool.linear1.weight", w1cf = "pool.linear1.weight#cf";
+    const int nb = (int)m.dim(w1, 0);
+    if (m.dim(w1, 1) != (int64_t)C * F || m.dim("pool.linear2.weight", 0) != (int64_t)C * F)
+      throw SpkError(SPK_E_WEIGHTS, "pool.linear1/2: in_dim != channels x frequency rows of the pooled map");
+    if (!m.uploaded && !m.W.count(w1cf)) {
+      Model::HostT t = m.get(w1);
+      t.shape = {nb, C, F, 1};
+      m.W[w1cf] = std::move(t);
+    }
+    const ChanMap bott = ChanMap::dense(nb);
+    const Packed& p1 = m.pack("pool.linear1", bott, {Part{w1cf, "pool.linear1.bias", "", ChanMap::dense(C, 1), 0, 0}}, F * C);
+    ChanMap fc;   // linear2 output: reference channel c*F + f -> column f*C + c
+    fc.n_phys = F * C;
+    fc.phys.resize((size_t)F * C);
+    for (int c = 0; c < C; ++c)
+      for (int f = 0; f < F; ++f) fc.phys[(size_t)c * F + f] = f * C + c;
+    const Packed& p2 = m.pack("pool.linear2", fc, {Part{"pool.linear2.weight", "pool.linear2.bias", "", bott, 0, 0}}, nb);
+    b.macs_per_utt += 2.0 * T * (double)C * F * nb;
+    if (!b.plan) return;
+    const int ldb = bott.n_phys;
+    const Buf A = b.alloc((size_t)B * T * ldb), L = b.alloc((size_t)B * T * F * C);
+    ConvDesc d1;
+    d1.nimg = B; d1.Ho = 1; d1.Wo = T;
+    d1.s0.ld = x.ld; d1.s0.H = F; d1.s0.W = T; d1.s0.cin = C;
+    d1.s0.kh = F; d1.s0.kw = 1;
+    d1.ldo = ldb; d1.act = ACT_TANH;
+    Builder::ConvIO io1; io1.s0 = x.buf; io1.out = A;
+    b.conv("pool.linear1", d1, p1, io1);
+    ConvDesc d2;
+    d2.nimg = B; d2.Ho = 1; d2.Wo = T;
+    d2.s0.ld = ldb; d2.s0.H = 1; d2.s0.W = T; d2.s0.cin = ldb;
+    d2.ldo = F * C;
+    Builder::ConvIO io2; io2.s0 = A; io2.out = L;
+    b.conv("pool.linear2", d2, p2, io2);
+    const T4 xx = x;
+    b.step("pool", [=](const Ctx& c) {
+      return launch_astp_pool(c.resolve(L), F * C, c.resolve(xx.buf), xx.ld, B, F, T, C, c.resolve(stats), c.stream);
+    });
+  }
+
   // AFF bottleneck layout: C/4 channels, up to 64 of them padded to a multiple of 32 (the
   // fused kernel's MFMA tiles; for the two-conv form the second conv's K-tile is one whole
   // tap, so the buffer-resource loader applies); padding channels have zero weights and
@@ -375,15 +422,18 @@ struct ERes2Builder {
     }
 
     // ---- TSTP (pooling_layers.py:47-55) -> stats [B, 2*H*C] in (h, c) order; TAP / TSDP
-    //      (:10-35, pooling_func) keep only the mean / the std part
+    //      (:10-35, pooling_func) keep only the mean / the std part; ASTP (:58-104) pools
+    //      with attention weights into the same (h, c) order
     const int pool = m.cfg.pooling;
-    if (pool < SPK_POOL_TSTP || pool > SPK_POOL_TSDP) throw SpkError(SPK_E_UNSUPPORTED, "pooling must be TSTP, TAP or TSDP");
+    if (pool < SPK_POOL_TSTP || pool > SPK_POOL_ASTP) throw SpkError(SPK_E_UNSUPPORTED, "pooling must be TSTP, TAP, TSDP or ASTP");
     const int parts = pool == SPK_POOL_TAP ? 1 : pool == SPK_POOL_TSDP ? 2 : 3;
     const int nst = parts == 3 ? 2 : 1;
     const int H4 = fused.H, C4 = fused.C;
     const int S = nst * H4 * C4;
     const Buf stats = b.alloc((size_t)B * S);
-    if (b.plan) {
+    if (pool == SPK_POOL_ASTP) {
+      astp(fused, stats);
+    } else if (b.plan) {
       const T4 f = fused;
       b.step("pool", [=](const Ctx& c) {
         return launch_tstp(c.resolve(f.buf), B, f.H, f.W, f.C, f.ld, 1e-8f, 1, c.resolve(stats), c.stream, parts);

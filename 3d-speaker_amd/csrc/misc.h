@@ -19,4 +19,9 @@ hipError_t launch_split_f16(const float* w, uint16_t* hi, uint16_t* lo, size_t n
 hipError_t launch_tstp(const float* x, int B, int H, int W, int C, int ld, float eps, int unbiased, float* out,
                        hipStream_t s, int parts = 3);
 
+// ASTP attentive statistics (pooling_layers.py:93-104): x [B, F, T, C] (pixel stride ldx),
+// logits [B, T, F*C] (column f*C + c, row stride ldl) -> out [B, 2*F*C] (mean, std; f*C + c order)
+hipError_t launch_astp_pool(const float* logit, int ldl, const float* x, int ldx, int B, int F, int T, int C,
+                            float* out, hipStream_t s);
+
 }  // namespace spk

@@ -114,7 +114,53 @@ tstp_kernel(const float* __restrict__ x, int B, int H, int W, int C, int ld, flo
   }
 }
 
+// ASTP pooling (pooling_layers.py:93-104) over x [B, F, T, C] (pixel stride ldx) with the
+// attention logits [B, T, F*C] (row stride ldl, column f*C + c): per (b, f, c) an online
+// softmax over time fused with a weighted Welford pass (x and the logits read once);
+// var = M2 / sum w (= sum alpha x^2 - mean^2), std = sqrt(max(var, 1e-10)).  out [B, 2*F*C]:
+// mean at f*C + c, std at F*C + f*C + c (the TSTP order seg_1 is packed for).
+__global__ void __launch_bounds__(256)
+astp_pool_kernel(const float* __restrict__ logit, int ldl, const float* __restrict__ x, int ldx, int B, int F, int T,
+                 int C, float* __restrict__ out, const int* __restrict__ run_if) {
+  SPK_GATE(run_if);
+  const long long total = (long long)B * F * C;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const int f = (int)((e / C) % F);
+    const int b = (int)(e / ((long long)C * F));
+    const float* l = logit + (size_t)b * T * ldl + (size_t)f * C + c;
+    const float* p = x + ((size_t)(b * F + f) * T) * ldx + c;
+    float mx = -INFINITY, sw = 0.f, mean = 0.f, m2 = 0.f;
+    for (int t = 0; t < T; ++t) {
+      const float lv = l[(size_t)t * ldl], xv = p[(size_t)t * ldx];
+      if (lv > mx) {
+        const float sc = __expf(mx - lv);   // 0 on the first sample
+        sw *= sc;
+        m2 *= sc;
+        mx = lv;
+      }
+      const float w = __expf(lv - mx);
+      sw += w;
+      const float d = xv - mean;
+      mean += d * (w / sw);
+      m2 += w * d * (xv - mean);
+    }
+    float* o = out + (size_t)b * 2 * F * C;
+    o[f * C + c] = mean;
+    o[F * C + f * C + c] = sqrtf(fmaxf(m2 / sw, 1e-10f));
+  }
+}
+
 }  // namespace
+
+hipError_t launch_astp_pool(const float* logit, int ldl, const float* x, int ldx, int B, int F, int T, int C,
+                            float* out, hipStream_t s) {
+  const long long total = (long long)B * F * C;
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 65536);
+  hipLaunchKernelGGL(astp_pool_kernel, dim3(blocks), dim3(256), 0, s, logit, ldl, x, ldx, B, F, T, C, out, launch_gate());
+  return hipGetLastError();
+}
 
 hipError_t launch_stem_conv3x3(const float* feats, int B, int T, int F, const float* w, const float* bias, int cout,
                                int act, int wstride, float* out, int ldo, hipStream_t s, const int* vlen,

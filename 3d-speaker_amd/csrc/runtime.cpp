@@ -583,7 +583,17 @@ static int enqueue_steps(const char* fn, const PlanPair& pp, const Ctx& base, bo
   };
   if (exact || !pp.x3) return run(*pp.ex, nullptr, nullptr);
   int* word = reinterpret_cast<int*>(base.ws + pp.stage_flag);
-  if (int rc = hip_check(launch_word_reset(word, base.stream), "range word reset")) return rc;
+  // diagnostics (tools/race_probe.py): SPK_WORD_RESET=memset zeroes the word with a
+  // 4-byte hipMemsetAsync (a memset node in the captured graph) instead of the kernel node
+  static const bool memset_reset = [] {
+    const char* e = std::getenv("SPK_WORD_RESET");
+    return e && std::string(e) == "memset";
+  }();
+  if (memset_reset) {
+    if (int rc = hip_check(hipMemsetAsync(word, 0, sizeof(int), base.stream), "range word memset")) return rc;
+  } else if (int rc = hip_check(launch_word_reset(word, base.stream), "range word reset")) {
+    return rc;
+  }
   if (int rc = run(*pp.x3, word, nullptr)) return rc;
   static const bool no_rerun = std::getenv("SPK_DIAG_NO_RERUN") != nullptr;   // diagnostics only
   if (no_rerun) return SPK_OK;

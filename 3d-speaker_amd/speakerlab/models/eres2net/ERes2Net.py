@@ -38,7 +38,7 @@ class ERes2Net(_hip.HipModuleMixin, nn.Module):
                  m_channels=32, feat_dim=80, embedding_size=192, pooling_func='TSTP', two_emb_layer=False):
         super().__init__()
         self.pooling_func = pooling_func
-        pooling_layers.pooling_code(pooling_func)   # TSTP / TAP / TSDP (ASTP raises)
+        pooling_layers.pooling_code(pooling_func)   # TSTP / TAP / TSDP / ASTP
         self.feat_dim, self.embedding_size, self.two_emb_layer = feat_dim, embedding_size, two_emb_layer
         self.m_channels = m_channels
         self.stats_dim = int(feat_dim / 8) * m_channels * 8

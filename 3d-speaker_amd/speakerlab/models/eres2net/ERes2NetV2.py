@@ -36,7 +36,7 @@ class ERes2NetV2(_hip.HipModuleMixin, nn.Module):
                  pooling_func='TSTP', two_emb_layer=False):
         super().__init__()
         self.pooling_func = pooling_func
-        pooling_layers.pooling_code(pooling_func)   # TSTP / TAP / TSDP (ASTP raises)
+        pooling_layers.pooling_code(pooling_func)   # TSTP / TAP / TSDP / ASTP
         self.feat_dim, self.embedding_size, self.two_emb_layer = feat_dim, embedding_size, two_emb_layer
         self.m_channels, self.baseWidth, self.scale, self.expansion = m_channels, baseWidth, scale, expansion
         self.stats_dim = int(feat_dim / 8) * m_channels * 8

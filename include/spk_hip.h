@@ -71,6 +71,7 @@ typedef struct {
 #define SPK_POOL_TSTP 0
 #define SPK_POOL_TAP 1
 #define SPK_POOL_TSDP 2
+#define SPK_POOL_ASTP 3
 
 typedef struct {
   int32_t arch;
@@ -89,7 +90,8 @@ typedef struct {
                              multiply, fp32 accumulation -- BASELINE config C3's reduced-
                              precision mode (cosine >= 0.9999 to the reference) */
   int32_t pooling;        /* ERes2Net*: pooling_func -- SPK_POOL_TSTP (0, default), SPK_POOL_TAP (1),
-                             SPK_POOL_TSDP (2) (pooling_layers.py:10-55); ASTP is not offered */
+                             SPK_POOL_TSDP (2), SPK_POOL_ASTP (3, global_context_att=False)
+                             (pooling_layers.py:10-104) */
   int32_t reserved[6];
 } spk_model_config_t;
 

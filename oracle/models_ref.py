@@ -11,7 +11,7 @@ layout) and restates the reference forward op for op with ``torch.nn.functional`
 * ERes2NetV2   — ``speakerlab/models/eres2net/ERes2NetV2.py:31-254``
 * ERes2Net     — ``speakerlab/models/eres2net/ERes2Net.py:30-231``
 * AFF          — ``speakerlab/models/eres2net/fusion.py:8-28``
-* TSTP         — ``speakerlab/models/eres2net/pooling_layers.py:38-55``
+* TSTP         — ``speakerlab/models/eres2net/pooling_layers.py:38-55`` (TAP / TSDP :10-35, ASTP :58-104)
 * ECAPA_TDNN   — ``speakerlab/models/ecapa_tdnn/ECAPA_TDNN.py:29-463``
 * CAMPPlus     — ``speakerlab/models/campplus/DTDNN.py:13-115``, ``layers.py:10-253``
 * ResNet34     — ``speakerlab/models/resnet/ResNet.py:15-113``
@@ -93,6 +93,18 @@ def _tstp(x, pooling='TSTP'):
     return torch.cat((mean, std), 1)
 
 
+def _astp(sd: SD, x, prefix='pool'):
+    """ASTP pooling_layers.py:58-104 (global_context_att=False): alpha = softmax_T(linear2(
+    tanh(linear1(x)))) over (C*F, T); mean = sum alpha x, std = sqrt(clamp(sum alpha x^2 -
+    mean^2, 1e-10)), cat(mean, std)."""
+    x = x.reshape(x.shape[0], x.shape[1] * x.shape[2], x.shape[3])
+    a = torch.tanh(F.conv1d(x, sd[f'{prefix}.linear1.weight'], sd[f'{prefix}.linear1.bias']))
+    a = torch.softmax(F.conv1d(a, sd[f'{prefix}.linear2.weight'], sd[f'{prefix}.linear2.bias']), dim=2)
+    mean = torch.sum(a * x, dim=2)
+    var = torch.sum(a * (x ** 2), dim=2) - mean ** 2
+    return torch.cat([mean, torch.sqrt(var.clamp(min=1e-10))], dim=1)
+
+
 def _eres2_layer(sd: SD, name: str, x, n_blocks: int, stride: int, width: int, scale: int, aff: bool):
     for b in range(n_blocks):
         x = _eres2_block(sd, f'{name}.{b}', x, stride if b == 0 else 1, width, scale, aff)
@@ -111,7 +123,8 @@ def eres2netv2_forward(sd: SD, x, m_channels=64, base_width=26, scale=2, num_blo
     out4 = _eres2_layer(sd, 'layer4', out3, num_blocks[3], 2, widths[3], scale, True)
     out3_ds = F.conv2d(out3, sd['layer3_ds.weight'], stride=2, padding=1)
     fused = _aff(sd, 'fuse34', out4, out3_ds)
-    emb = F.linear(_tstp(fused, pooling), sd['seg_1.weight'], sd['seg_1.bias'])
+    stats = _astp(sd, fused) if pooling == 'ASTP' else _tstp(fused, pooling)
+    emb = F.linear(stats, sd['seg_1.weight'], sd['seg_1.bias'])
     if two_emb_layer:
         emb = F.linear(_bn(F.relu(emb), sd, 'seg_bn_1'), sd['seg_2.weight'], sd['seg_2.bias'])
     return emb

@@ -199,6 +199,27 @@ hipError_t launch_tstp(const float* x, int B, int H, int W, int C, int ld, float
   return hipSuccess;
 }
 
+hipError_t launch_astp_pool(const float* logit, int ldl, const float* x, int ldx, int B, int F, int T, int C, float* out,
+                            hipStream_t) {
+  EMU_GATE();
+  for (int b = 0; b < B; ++b)
+    for (int f = 0; f < F; ++f)
+      for (int c = 0; c < C; ++c) {
+        double mx = -1e300;
+        for (int t = 0; t < T; ++t) mx = std::max(mx, (double)logit[((size_t)b * T + t) * ldl + f * C + c]);
+        double sw = 0, s1 = 0, s2 = 0;
+        for (int t = 0; t < T; ++t) {
+          const double w = std::exp((double)logit[((size_t)b * T + t) * ldl + f * C + c] - mx);
+          const double v = x[((size_t)(b * F + f) * T + t) * ldx + c];
+          sw += w; s1 += w * v; s2 += w * v * v;
+        }
+        const double mean = s1 / sw, var = s2 / sw - mean * mean;
+        out[(size_t)b * 2 * F * C + f * C + c] = (float)mean;
+        out[(size_t)b * 2 * F * C + F * C + f * C + c] = (float)std::sqrt(std::max(var, 1e-10));
+      }
+  return hipSuccess;
+}
+
 hipError_t launch_fbank(const float*, const int64_t*, int, float*, const int64_t*, int, int, const FbankTables*, int,
                         hipStream_t, int) {
   EMU_GATE();

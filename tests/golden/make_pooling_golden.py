@@ -1,5 +1,5 @@
-"""Reference goldens for the TAP / TSDP pooling heads of ERes2NetV2 (pooling_func,
-``speakerlab/models/eres2net/pooling_layers.py:10-35``, ``ERes2NetV2.py:215-217``).
+"""Reference goldens for the TAP / TSDP / ASTP pooling heads of ERes2NetV2 (pooling_func,
+``speakerlab/models/eres2net/pooling_layers.py:10-35, 58-104``, ``ERes2NetV2.py:215-217``).
 
 Run in the build container only:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_pooling_golden.py
 
@@ -22,7 +22,7 @@ def main():
     bn = dict(np.load(os.path.join(HERE, 'eres2netv2_bn.npz')))
     _, feats = mg.feats_for(2, 16000, 21)
     out = {'feats': feats}
-    for pool in ('TAP', 'TSDP'):
+    for pool in ('TAP', 'TSDP', 'ASTP'):
         model = mg.ERes2NetV2(feat_dim=80, embedding_size=192, pooling_func=pool)
         mg.synthetic.load_synthetic_weights(model, seed=0, bn_stats=bn)
         model.eval()
