@@ -8,7 +8,7 @@ LIBS=${LIBS:-"ab/libspk_head.so 3d-speaker_amd/lib/libspk_hip.so"}
 for arch in ${ARCHS:-eres2netv2 eres2net_large}; do
   for rep in $(seq 1 ${REPS:-2}); do
     for ent in $LIBS; do
-      lib=${ent%%:*}; envs=""; [ "$ent" != "$lib" ] && envs=${ent#*:}
+      lib=${ent%%:*}; envs=""; [ "$ent" != "$lib" ] && envs=${ent#*:}; envs=${envs//,/ }
       tag=$(basename $lib .so)${envs:+_${envs//[^A-Za-z0-9]/}}
       env $envs SPK_HIP_LIB=$lib timeout -k 10 300 python tools/profile_steps.py --arch $arch --json gpurun_out/ab_${arch}_${tag}_${rep}.json > gpurun_out/ab_${arch}_${tag}_${rep}.txt 2>&1
       rc=$?; echo "$tag/$rep $(grep -v amdgpu.ids gpurun_out/ab_${arch}_${tag}_${rep}.txt | head -1)"
