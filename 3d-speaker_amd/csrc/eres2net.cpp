@@ -53,6 +53,21 @@ struct ERes2Builder {
   int scale, expansion;
   double base_width;
   Buf T1, CAT, MID, FB;   // block scratch, sized for the largest layer
+  // fp16x3 range guard by segment (runtime.h Plan::seg_end): the plan is cut after every block
+  // and once at the end; a segment needs its gated exact twin only if a split-GEMM operand in
+  // it has no static bound below kRangeLimit.  Bounds: Hardtanh(0, 20) outputs (every block
+  // output and every in-block activation), |AFF| <= 2 max(|x|, |y|), a conv's |W x + b| <=
+  // max_n sum_k |w_nk| |x|max + |b|max from the packed weights; the stem output (ReLU of the
+  // model input's conv) has none, so the first block's segment keeps its twin.
+  static constexpr double kHt = 20.0;
+  bool seg_hot = false;
+  void need(double bound) {
+    if (!(bound < (double)kRangeLimit)) seg_hot = true;
+  }
+  void close_segment() {
+    b.segment(seg_hot);
+    seg_hot = false;
+  }
 
   ERes2Builder(Builder& bb, bool isv2) : b(bb), m(bb.m), v2(isv2) {
     // ERes2Net (ERes2Net.py) fixes scale 2 / expansion 2 / baseWidth 32; ERes2Net_huge
@@ -119,7 +134,8 @@ struct ERes2Builder {
   static ChanMap aff_mid(int C) { return ChanMap::dense(C / 4, C / 4 <= 64 ? 32 : 4); }
 
   // AFF(x, y) -> out (fusion.py:22-28); x, y, out share geometry, C logical channels each.
-  void aff(const std::string& p, const T4& x, const T4& y, int C, const T4& out) {
+  // |x| <= bx, |y| <= by; returns the bound of |out|.
+  double aff(const std::string& p, const T4& x, const T4& y, int C, const T4& out, double bx, double by) {
     const int inter = C / 4;
     const ChanMap xin = ChanMap::dense(C);
     const int cp = xin.n_phys;
@@ -132,9 +148,13 @@ struct ERes2Builder {
                               {Part{p + ".local_att.3.weight", p + ".local_att.3.bias", p + ".local_att.4", mid, 0, 0}},
                               mid.n_phys);
     const double m0 = pix(x) * 2.0 * C * inter, m3 = pix(x) * (double)inter * C;
+    const double bin = std::max(bx, by);
+    need(bin);                                  // local_att.0 reads cat(x, y)
+    need(Builder::bound(a0, bin));              // local_att.3 reads SiLU(BN(local_att.0)): |silu z| <= |z|
+    const double bout = 2.0 * bin;
     if (!b.plan) {
       b.macs_per_utt += m0 + m3;
-      return;
+      return bout;
     }
     if (b.x3() && aff_x3_supported(cp, mid.n_phys)) {
       // one fused kernel (aff.hip): x and y read once, h never leaves registers
@@ -157,7 +177,7 @@ struct ERes2Builder {
         ad.range_flag = c.flag;
         return launch_aff_x3(ad, c.stream);
       }, aff_x3_kernel_name(mid.n_phys), bytes);
-      return;
+      return bout;
     }
     b.macs_per_utt += m0;
     ConvDesc d;
@@ -178,6 +198,7 @@ struct ERes2Builder {
     io2.s0 = MID; io2.out = out.buf; io2.affx = x.buf; io2.affy = y.buf;
     b.macs_per_utt += m3;
     b.conv(p + ".local_att.3", e, a1, io2);
+    return bout;
   }
 
   // The whole block as one fused kernel (res2block.hip / res2block_s2.hip), scale 2, fp16x3
@@ -242,9 +263,11 @@ struct ERes2Builder {
     return true;
   }
 
-  T4 block(const std::string& p, const T4& x, int stride, int width, int planes, bool use_aff, Buf outbuf) {
+  // |x| <= bx; the block's output is Hardtanh-bounded (kHt)
+  T4 block(const std::string& p, const T4& x, int stride, int width, int planes, bool use_aff, Buf outbuf, double bx) {
     const int Ho = (x.H - 1) / stride + 1, Wo = (x.W - 1) / stride + 1;
     const int Cout = planes * expansion;
+    need(bx);                                   // conv1 and the shortcut read x; T1 / CAT are Hardtanh outputs
     T4 fo;
     if (fusable(p, x, stride, width, Cout, use_aff) && fused_block(p, x, stride, width, Cout, outbuf, fo)) return fo;
     const ChanMap sl = ChanMap::slices(width, scale);
@@ -275,7 +298,7 @@ struct ERes2Builder {
         T4 prev{CAT.at((size_t)(i - 1) * wp), ldt, Ho, Wo, wp};
         if (use_aff) {
           T4 f{FB, wp, Ho, Wo, wp};
-          aff(p + ".fuse_models." + std::to_string(i - 1), prev, in, width, f);
+          aff(p + ".fuse_models." + std::to_string(i - 1), prev, in, width, f, kHt, kHt);
           in = f;
         } else {
           addend = prev.buf;
@@ -337,6 +360,7 @@ struct ERes2Builder {
     // ---- stem conv 3x3 1->mc + bn1 + relu (ERes2NetV2.py:238)
     const Packed& stem = m.pack("conv1", ChanMap::dense(mc), {Part{"conv1.weight", "", "bn1", ChanMap::dense(1, 1), 0, 0}}, 9);
     T4 x{b.alloc((size_t)B * F * T * mc), mc, F, T, mc};
+    double bx = INFINITY;   // ReLU(BN(conv(input))): no static bound
     b.macs_per_utt += (double)F * T * mc * 9;
     if (b.plan) {
       const float* w = m.dptr(stem.w_off);
@@ -381,18 +405,24 @@ struct ERes2Builder {
       const int Ho = (x.H - 1) / stride + 1, Wo = (x.W - 1) / stride + 1;
       const size_t osz = (size_t)B * Ho * Wo * ChanMap::dense(planes * expansion).n_phys;
       Buf pp[2] = {b.alloc(osz), b.alloc(osz)};
-      for (int bi = 0; bi < nb; ++bi)
-        x = block(layer + "." + std::to_string(bi), x, bi ? 1 : stride, width, planes, li >= 2, pp[bi & 1]);
+      for (int bi = 0; bi < nb; ++bi) {
+        x = block(layer + "." + std::to_string(bi), x, bi ? 1 : stride, width, planes, li >= 2, pp[bi & 1], bx);
+        bx = kHt;
+        close_segment();   // the stem's segment ends with layer1.0
+      }
       outs[li] = x;
     }
 
     T4 fused;
-    auto downsample = [&](const std::string& key, const T4& in) {
+    double bnd = 0.0;   // bound of the last downsample / fuse output
+    auto downsample = [&](const std::string& key, const T4& in, double bin) {
       const int Cout = (int)m.dim(key, 0);
       const ChanMap om = ChanMap::dense(Cout);
       const Packed& p = m.pack(key, om, {Part{key, "", "", ChanMap::dense(in.C), 0, 0}}, 9 * in.C);
       const int Ho = (in.H - 1) / 2 + 1, Wo = (in.W - 1) / 2 + 1;
       T4 out{b.alloc((size_t)B * Ho * Wo * om.n_phys), om.n_phys, Ho, Wo, om.n_phys};
+      need(bin);
+      bnd = p.l1max * bin;   // no bias
       b.macs_per_utt += (double)Ho * Wo * Cout * in.C * 9.0;
       if (b.plan) {
         ConvDesc d;
@@ -404,22 +434,23 @@ struct ERes2Builder {
       }
       return out;
     };
-    auto fuse = [&](const std::string& key, const T4& a, const T4& y) {
+    auto fuse = [&](const std::string& key, const T4& a, const T4& y, double by) {
       T4 out{b.alloc((size_t)B * a.H * a.W * a.C), a.C, a.H, a.W, a.C};
-      aff(key, a, y, a.C, out);
+      bnd = aff(key, a, y, a.C, out, kHt, by);
       return out;
     };
     if (v2) {
-      const T4 ds = downsample("layer3_ds.weight", outs[2]);
-      fused = fuse("fuse34", outs[3], ds);
+      const T4 ds = downsample("layer3_ds.weight", outs[2], kHt);
+      fused = fuse("fuse34", outs[3], ds, bnd);
     } else {
-      const T4 d1 = downsample("layer1_downsample.weight", outs[0]);
-      const T4 f12 = fuse("fuse_mode12", outs[1], d1);
-      const T4 d2 = downsample("layer2_downsample.weight", f12);
-      const T4 f123 = fuse("fuse_mode123", outs[2], d2);
-      const T4 d3 = downsample("layer3_downsample.weight", f123);
-      fused = fuse("fuse_mode1234", outs[3], d3);
+      const T4 d1 = downsample("layer1_downsample.weight", outs[0], kHt);
+      const T4 f12 = fuse("fuse_mode12", outs[1], d1, bnd);
+      const T4 d2 = downsample("layer2_downsample.weight", f12, bnd);
+      const T4 f123 = fuse("fuse_mode123", outs[2], d2, bnd);
+      const T4 d3 = downsample("layer3_downsample.weight", f123, bnd);
+      fused = fuse("fuse_mode1234", outs[3], d3, bnd);
     }
+    const double bfused = bnd;   // pooled statistics (mean, std, attention-weighted too) stay below it
 
     // ---- TSTP (pooling_layers.py:47-55) -> stats [B, 2*H*C] in (h, c) order; TAP / TSDP
     //      (:10-35, pooling_func) keep only the mean / the std part; ASTP (:58-104) pools
@@ -431,6 +462,7 @@ struct ERes2Builder {
     const int H4 = fused.H, C4 = fused.C;
     const int S = nst * H4 * C4;
     const Buf stats = b.alloc((size_t)B * S);
+    need(bfused);   // ASTP linear1 (its linear2 reads tanh outputs) or seg_1 reads the pooled stats
     if (pool == SPK_POOL_ASTP) {
       astp(fused, stats);
     } else if (b.plan) {
@@ -473,6 +505,8 @@ struct ERes2Builder {
     }
     if (two) {
       const Packed& seg2 = m.pack("seg_2", em, {Part{"seg_2.weight", "seg_2.bias", "", ChanMap::dense(E, 1), 0, 0}}, E);
+      // seg_2 reads seg_bn_1(ReLU(seg_1(stats)))
+      need(Builder::bound(m.pack_post_affine("seg_bn_1", "seg_bn_1", em), Builder::bound(seg1, bfused)));
       b.macs_per_utt += (double)E * E;
       if (b.plan) {
         ConvDesc d;
@@ -484,6 +518,7 @@ struct ERes2Builder {
         b.conv("seg_2", d, seg2, io);
       }
     }
+    close_segment();
   }
 };
 

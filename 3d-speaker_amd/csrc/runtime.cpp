@@ -149,6 +149,12 @@ const Packed& Model::pack(const std::string& name, const ChanMap& out, const std
   }
   std::vector<float> wf(wd.begin(), wd.end()), bf(bd.begin(), bd.end());
   for (float v : wf) p.wmax = std::max(p.wmax, std::fabs(v));
+  for (int n = 0; n < N; ++n) {
+    double l1 = 0.0;
+    for (int k = 0; k < Kp; ++k) l1 += std::fabs((double)wf[(size_t)n * Kp + k]);
+    p.l1max = std::max(p.l1max, l1);
+    p.bmax = std::max(p.bmax, std::fabs((double)bf[n]));
+  }
   gemm_wmax = std::max(gemm_wmax, p.wmax);   // range guard (common.h)
   p.w_off = put(wf);
   p.b_off = put(bf);
@@ -166,6 +172,10 @@ const Packed& Model::pack_post_affine(const std::string& name, const std::string
   for (int c = 0; c < out.n_log(); ++c) { ps[out.phys[c]] = (float)s[c]; pt[out.phys[c]] = (float)t[c]; }
   Packed p;
   p.N = out.n_phys;
+  for (int c = 0; c < out.n_phys; ++c) {   // |s x + t| <= l1max |x| + bmax (Builder::bound)
+    p.l1max = std::max(p.l1max, std::fabs((double)ps[c]));
+    p.bmax = std::max(p.bmax, std::fabs((double)pt[c]));
+  }
   p.ps_off = put(ps);
   p.pt_off = put(pt);
   return packed.emplace(key, p).first->second;
@@ -176,7 +186,14 @@ Buf Builder::alloc(size_t floats) {
   b.kind = Buf::WS;
   b.off = ws;
   ws += (floats * sizeof(float) + 255) / 256 * 256;
+  if (plan) plan->allocs.emplace_back(b.off, floats);
   return b;
+}
+
+void Builder::segment(bool twin) {
+  if (!plan) return;
+  plan->seg_end.push_back(plan->steps.size());
+  plan->seg_twin.push_back(twin ? 1 : 0);
 }
 
 void Builder::step(const std::string& name, Step s, const std::string& kernel, double bytes) {
@@ -562,17 +579,30 @@ static bool use_graphs() {
   return on;
 }
 
+// Both plans of the pair are cut into the same segments, every segment ends on the last
+// step, and they lay the workspace out alike (a twin then writes exactly the buffers its
+// split segment wrote); SPK_GUARD_SEGMENTS=0 forces the whole-plan twin (A/B, diagnostics)
+static bool segmented(const PlanPair& pp) {
+  static const bool on = [] {
+    const char* e = std::getenv("SPK_GUARD_SEGMENTS");
+    return !(e && std::string(e) == "0");
+  }();
+  const Plan &x = *pp.x3, &e = *pp.ex;
+  return on && !x.seg_end.empty() && x.seg_end.size() == e.seg_end.size() && x.seg_end.back() == x.steps.size() &&
+         e.seg_end.back() == e.steps.size() && x.allocs == e.allocs;
+}
+
 // Enqueue one forward: the range word is zeroed, the fp16x3 plan runs (its producers note
 // range overflows in the word), then the exact-fp32 plan runs with every launch gated on the
 // word (common.h SPK_GATE): a batch whose activations left fp16's range is recomputed on the
 // exact kernels and overwrites the embeddings, all on `stream`, with no host round trip.
 // `exact` runs the exact plan alone (spk_model_forward_exact).
 static int enqueue_steps(const char* fn, const PlanPair& pp, const Ctx& base, bool exact) {
-  auto run = [&](const Plan& p, int* flag, const int* gate) -> int {
+  auto run = [&](const Plan& p, size_t i0, size_t i1, int* flag, const int* gate) -> int {
     Ctx c = base;
     c.flag = flag;
     GateScope g(gate);
-    for (size_t i = 0; i < p.steps.size(); ++i) {
+    for (size_t i = i0; i < i1; ++i) {
       hipError_t e = p.steps[i](c);
       if (e != hipSuccess) {
         set_error(std::string(fn) + ": step '" + p.names[i] + "': " + hipGetErrorString(e));
@@ -581,7 +611,7 @@ static int enqueue_steps(const char* fn, const PlanPair& pp, const Ctx& base, bo
     }
     return SPK_OK;
   };
-  if (exact || !pp.x3) return run(*pp.ex, nullptr, nullptr);
+  if (exact || !pp.x3) return run(*pp.ex, 0, pp.ex->steps.size(), nullptr, nullptr);
   int* word = reinterpret_cast<int*>(base.ws + pp.stage_flag);
   // diagnostics (tools/race_probe.py): SPK_WORD_RESET=memset zeroes the word with a
   // 4-byte hipMemsetAsync (a memset node in the captured graph) instead of the kernel node
@@ -594,10 +624,23 @@ static int enqueue_steps(const char* fn, const PlanPair& pp, const Ctx& base, bo
   } else if (int rc = hip_check(launch_word_reset(word, base.stream), "range word reset")) {
     return rc;
   }
-  if (int rc = run(*pp.x3, word, nullptr)) return rc;
   static const bool no_rerun = std::getenv("SPK_DIAG_NO_RERUN") != nullptr;   // diagnostics only
+  if (segmented(pp)) {
+    // segment by segment: a segment's exact twin, gated on the word, follows it only where one
+    // of its split-GEMM operands is not statically bounded below kRangeLimit (Builder::segment);
+    // a flagged segment is recomputed before any later segment reads its outputs
+    const Plan &x = *pp.x3, &e = *pp.ex;
+    for (size_t sgi = 0; sgi < x.seg_end.size(); ++sgi) {
+      const size_t x0 = sgi ? x.seg_end[sgi - 1] : 0, e0 = sgi ? e.seg_end[sgi - 1] : 0;
+      if (int rc = run(x, x0, x.seg_end[sgi], word, nullptr)) return rc;
+      if (x.seg_twin[sgi] && !no_rerun)
+        if (int rc = run(e, e0, e.seg_end[sgi], nullptr, word)) return rc;
+    }
+    return SPK_OK;
+  }
+  if (int rc = run(*pp.x3, 0, pp.x3->steps.size(), word, nullptr)) return rc;
   if (no_rerun) return SPK_OK;
-  return run(*pp.ex, nullptr, word);
+  return run(*pp.ex, 0, pp.ex->steps.size(), nullptr, word);
 }
 
 // Replay the forward as one hipGraph: inputs are copied into the workspace's staging regions,
@@ -704,6 +747,32 @@ int spk_model_forward_lengths(spk_model_t* model, const float* feats, int32_t B,
   return guarded([&]() -> int {
     return run_forward("spk_model_forward_lengths", model, feats, B, T, lengths, workspace, workspace_bytes, emb_out,
                        stream);
+  });
+}
+
+int spk_model_guard_plan(spk_model_t* model, int32_t B, int32_t T, int32_t ragged, int32_t* n_segments,
+                         int32_t* n_twin_segments, int32_t* n_gated_steps) {
+  return guarded([&]() -> int {
+    if (!model || B <= 0 || T <= 0 || !n_segments || !n_twin_segments || !n_gated_steps) {
+      set_error("spk_model_guard_plan: invalid argument");
+      return SPK_E_INVALID;
+    }
+    std::shared_ptr<PlanPair> pp = get_pair(model, B, T, ragged != 0);
+    *n_segments = *n_twin_segments = *n_gated_steps = 0;
+    if (!pp->x3) return SPK_OK;
+    if (!segmented(*pp)) {
+      *n_segments = *n_twin_segments = 1;
+      *n_gated_steps = (int32_t)pp->ex->steps.size();
+      return SPK_OK;
+    }
+    const Plan& e = *pp->ex;
+    *n_segments = (int32_t)e.seg_end.size();
+    for (size_t i = 0; i < e.seg_end.size(); ++i)
+      if (pp->x3->seg_twin[i]) {
+        ++*n_twin_segments;
+        *n_gated_steps += (int32_t)(e.seg_end[i] - (i ? e.seg_end[i - 1] : 0));
+      }
+    return SPK_OK;
   });
 }
 

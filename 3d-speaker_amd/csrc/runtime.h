@@ -59,6 +59,13 @@ struct Plan {
   std::vector<double> flops;        // algorithmic FLOPs of the step (whole batch)
   std::vector<double> bytes;        // algorithmic HBM bytes of the step (each operand once; 0 = not priced)
   size_t ws_bytes = 0;              // intermediates (the pair adds staging, PlanPair)
+  // range-guard segments (Builder::segment): step ranges [seg_end[i-1], seg_end[i]) and whether
+  // the segment's exact twin must follow it (a split-GEMM operand of the segment is not proved
+  // below kRangeLimit); empty = one segment, twin always.  `allocs` logs the workspace layout,
+  // so the runtime can check that both plans of a pair place every buffer alike
+  std::vector<size_t> seg_end;
+  std::vector<char> seg_twin;
+  std::vector<std::pair<size_t, size_t>> allocs;
 };
 
 // A shape's fp16x3 plan and exact-fp32 plan over one workspace layout: intermediates in
@@ -94,6 +101,8 @@ struct Packed {
   size_t ps_off = SIZE_MAX, pt_off = SIZE_MAX;   // optional post-activation affine
   bool has_bias = false;
   float wmax = 0.f;                               // max |w| of the packed matrix
+  double l1max = 0.0;                             // max over output channels of sum_k |w| (bounds)
+  double bmax = 0.0;                              // max |bias|
   int kcb = 0;                                    // K order (common.h ConvDesc::kcb)
 };
 
@@ -167,6 +176,11 @@ struct Builder {
   bool x3() const { return !exact && conv_use_x3(); }
   Buf alloc(size_t floats);
   void step(const std::string& name, Step s, const std::string& kernel = "", double bytes = 0.0);
+  // close a range-guard segment at the current step (Plan::seg_end); `twin`: the gated
+  // exact twin of the segment must run behind it (models without segments: one segment, twin)
+  void segment(bool twin);
+  // static bound of a conv's output |W x + b| given |x| <= in (kRangeLimit analysis)
+  static double bound(const Packed& p, double in) { return p.l1max * in + p.bmax; }
   // emit an implicit-GEMM conv; pointers of `d` are taken from the Bufs
   struct ConvIO {
     Buf s0, s0b, s1, out, res, affx, affy, gate, partial, rowbias;

@@ -74,6 +74,9 @@ SYMBOLS = {
                                              ctypes.POINTER(ctypes.c_int32)]),
     'spk_model_forward_exact': (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_size_t, _P,
                                                _P]),
+    'spk_model_guard_plan': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                            ctypes.POINTER(ctypes.c_int32)]),
     'spk_model_plan_size': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
     'spk_model_plan_step': (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p,
                                            ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32,
@@ -371,6 +374,14 @@ class NativeModel:
             _check(lib().spk_model_range_check(self.handle, B, T, ragged, ws.data_ptr(), stream, ctypes.byref(flag)),
                    'spk_model_range_check')
         return bool(flag.value)
+
+    def guard_plan(self, B: int, T: int, ragged: bool = False) -> dict:
+        """How the guarded forward of shape (B, T) is cut into range-guard segments and how
+        many exact-plan launches are enqueued behind it (include/spk_hip.h spk_model_guard_plan)."""
+        vals = [ctypes.c_int32(0) for _ in range(3)]
+        _check(lib().spk_model_guard_plan(self.handle, B, T, int(ragged), *[ctypes.byref(v) for v in vals]),
+               'spk_model_guard_plan')
+        return dict(zip(('segments', 'twin_segments', 'gated_steps'), (v.value for v in vals)))
 
 
 class HipModuleMixin:

@@ -157,6 +157,15 @@ int spk_model_range_check(spk_model_t* model, int32_t B, int32_t T, int32_t ragg
                           void* stream, int32_t* overflowed);
 int spk_model_forward_exact(spk_model_t* model, const float* feats, int32_t B, int32_t T, const int32_t* lengths,
                             void* workspace, size_t workspace_bytes, float* emb_out, void* stream);
+/* How the guarded forward of shape (B, T, ragged) is cut (diagnostics, tests): the exact
+ * re-run is captured per segment of the plan, right behind the segment it can replace, and
+ * only for segments with a split-GEMM operand not statically bounded below 2^14 (ERes2Net*:
+ * Hardtanh / weight-norm bounds leave only the stem's segment; other models: one segment,
+ * the whole plan).  n_segments: segments of the plan; n_twin_segments: those with an exact
+ * twin; n_gated_steps: launches of the exact plan enqueued behind every guarded forward
+ * (no-ops unless the range word is set); 0 / 0 / 0 for an exact-only handle. */
+int spk_model_guard_plan(spk_model_t* model, int32_t B, int32_t T, int32_t ragged, int32_t* n_segments,
+                         int32_t* n_twin_segments, int32_t* n_gated_steps);
 
 /* Algorithmic FLOPs per utterance of T frames (2 x conv/linear MACs). */
 int spk_model_flops(spk_model_t* model, int32_t T, double* flops);

@@ -103,3 +103,48 @@ def test_weights_out_of_fp16_range_force_exact():
     assert helpers.rel_err(out, ref).max() < 1e-4
     steps = em.plan(1, feats.shape[1])
     assert not any(s[0] == 'range_in' for s in steps)           # the exact plan has no input check
+
+
+def _guard_plan(em, B, T, ragged=0):
+    v = [ctypes.c_int32(-1) for _ in range(3)]
+    _check(lib().spk_model_guard_plan(em.handle, B, T, ragged, *[ctypes.byref(x) for x in v]), 'guard_plan')
+    return [x.value for x in v]
+
+
+def test_eres2net_guard_segments_only_the_stem_segment_is_twinned():
+    """ERes2NetV2: every split-GEMM operand past the stem is bounded statically (Hardtanh(0, 20)
+    block outputs, |AFF| <= 2 max(|x|, |y|), weight-norm bounds of the downsample / AFF / seg
+    layers), so of the plan's segments (one per block, plus the tail) only the first -- the
+    stem and layer1.0, which read the unbounded stem output -- and, where the weight-norm
+    bound of fuse34's hidden layer (here 34.8 x 1130) passes 2^14, the tail get a gated
+    exact twin: about a dozen no-op launches behind a forward instead of the ~60-step plan."""
+    em = EmuModel(helpers.loaded_module('eres2netv2'))
+    nseg, ntwin, ngated = _guard_plan(em, 2, 40)
+    assert nseg == 3 + 4 + 6 + 3 + 1
+    assert 1 <= ntwin <= 2
+    assert 0 < ngated <= 14
+
+
+def test_eres2net_hot_input_reruns_the_stem_segment():
+    """An input value that drives the stem output past the range limit sets the word; the
+    first segment's exact twin recomputes stem + layer1.0 before layer1.1 reads its output,
+    and the embeddings match the fp64 reference."""
+    g = helpers.golden('eres2netv2')
+    m = helpers.loaded_module('eres2netv2')
+    feats = torch.from_numpy(g['feats2'][:1, :40]).clone()
+    feats[0, 7, 11] = 3.0e6
+    em = EmuModel(m)
+    out = em(feats).numpy()
+    assert _flag(em) == 1
+    sd = {k: v.double() if v.is_floating_point() else v for k, v in m.state_dict().items()}
+    ref = models_ref.forward('eres2netv2', sd, feats.double()).numpy()
+    assert helpers.rel_err(out, ref).max() < 1e-4
+
+
+def test_unbounded_models_keep_one_twinned_segment():
+    """ECAPA / CAM++ activations are unbounded (ReLU -> BN): the whole exact plan stays gated
+    behind the whole split plan."""
+    for arch in ('ecapa', 'campplus'):
+        em = EmuModel(helpers.loaded_module(arch))
+        nseg, ntwin, ngated = _guard_plan(em, 1, 40)
+        assert nseg == 1 and ntwin == 1 and ngated > 20

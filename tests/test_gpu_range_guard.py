@@ -131,3 +131,27 @@ def test_large_weights_take_exact_gemm_layer():
     ref32 = models_ref.forward(arch, m.cpu().state_dict(), feats).numpy()
     tol = max(1e-4, 2 * helpers.rel_err(ref32, ref).max())
     assert helpers.rel_err(out, ref).max() < tol, (helpers.rel_err(out, ref).max(), tol)
+
+
+def test_eres2net_hot_input_reruns_only_the_stem_segment():
+    """ERes2NetV2 is cut into range-guard segments (one per block + the tail); a model input
+    that drives the stem output past the limit is recomputed by the first segment's exact
+    twin before layer1.1 reads it, and the embeddings match fp64; a clean batch pays only the
+    few gated launches of the twinned segments."""
+    arch = 'eres2netv2'
+    g = helpers.golden(arch)
+    m = helpers.loaded_module(arch)
+    feats = torch.from_numpy(g['feats2'][:3]).clone()
+    feats[1, 7, 11] = 3.0e6
+    sd = {k: v.double() if v.is_floating_point() else v for k, v in m.state_dict().items()}
+    ref = models_ref.forward(arch, sd, feats.double()).numpy()
+    dev = torch.device('cuda', 0)
+    m = m.to(dev)
+    with torch.no_grad():
+        out = m(feats.to(dev)).cpu().numpy()
+    h = m._hip_handle(dev)
+    assert h.last_forward_exact
+    assert helpers.rel_err(out, ref).max() < 1e-4
+    B, T, _ = feats.shape
+    gp = h.guard_plan(B, T)
+    assert gp['segments'] == 17 and 1 <= gp['twin_segments'] <= 2 and gp['gated_steps'] <= 14
