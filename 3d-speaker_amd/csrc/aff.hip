@@ -33,14 +33,11 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void split8(const f32x4 a, const f32x4 b, f16x8& hi, f16x8& lo) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const _Float16 ha = (_Float16)a[e], hb = (_Float16)b[e];
-    hi[e] = ha;
-    hi[e + 4] = hb;
-    lo[e] = (_Float16)((a[e] - (float)ha) * 2048.0f);
-    lo[e + 4] = (_Float16)((b[e] - (float)hb) * 2048.0f);
-  }
+  h16x4 ha, la, hb, lb;
+  split_x3(a, ha, la);
+  split_x3(b, hb, lb);
+  hi = f16x8{ha[0], ha[1], ha[2], ha[3], hb[0], hb[1], hb[2], hb[3]};
+  lo = f16x8{la[0], la[1], la[2], la[3], lb[0], lb[1], lb[2], lb[3]};
 }
 
 __device__ __forceinline__ f16x8 ld_h8(const uint16_t* p) { return *reinterpret_cast<const f16x8*>(p); }

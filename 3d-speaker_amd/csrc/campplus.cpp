@@ -84,13 +84,18 @@ void build_campplus(Builder& b, int T) {
       A4 out{b.alloc((size_t)B * Ho * T * mc), mc, Ho, T, mc};
       const Packed& c1 = m.pack(p + ".conv1", cm, {Part{p + ".conv1.weight", "", p + ".bn1", cm, 0, 0}}, 9 * mc);
       const bool sc = m.has(p + ".shortcut.0.weight");
-      std::vector<Part> parts{Part{p + ".conv2.weight", "", p + ".bn2", cm, 0, 0}};
-      if (sc) parts.push_back(Part{p + ".shortcut.0.weight", "", p + ".shortcut.1", cm, 0, 9 * mc});
-      const Packed& c2 = m.pack(p + ".conv2", cm, parts, 9 * mc + (sc ? mc : 0));
+      // the projection shortcut (1x1, frequency stride 2, + BN) is its own small GEMM whose
+      // output conv2 adds as a residual: conv2 is then a plain stride-1 3x3 conv that the
+      // halo kernel takes, instead of an implicit GEMM with a K-concatenated operand on
+      // 32-wide tiles
+      const Packed& c2 = m.pack(p + ".conv2", cm, {Part{p + ".conv2.weight", "", p + ".bn2", cm, 0, 0}}, 9 * mc);
+      const Packed* csc = sc ? &m.pack(p + ".shortcut", cm, {Part{p + ".shortcut.0.weight", "", p + ".shortcut.1", cm, 0, 0}}, mc)
+                             : nullptr;
+      A4 scb{sc ? b.alloc((size_t)B * Ho * T * mc) : Buf{}, mc, Ho, T, mc};
       const double macs1 = (double)Ho * T * mc * mc * 9;
-      const double macs2 = macs1 + (sc ? (double)Ho * T * mc * mc : 0.0);
+      const double macs_sc = sc ? (double)Ho * T * mc * mc : 0.0;
       b.macs_per_utt += macs1;
-      if (!b.plan) b.macs_per_utt += macs2;
+      if (!b.plan) b.macs_per_utt += macs1 + macs_sc;
       if (b.plan) {
         ConvDesc d;
         d.nimg = B; d.Ho = Ho; d.Wo = T;
@@ -98,18 +103,23 @@ void build_campplus(Builder& b, int T) {
         d.ldo = mc; d.act = ACT_RELU;
         Builder::ConvIO io; io.s0 = x.buf; io.out = y1.buf; io.rowlen = LENS;
         b.conv(p + ".conv1", d, c1, io);
-        b.macs_per_utt += macs2;
+        if (sc) {
+          b.macs_per_utt += macs_sc;
+          ConvDesc f;
+          f.nimg = B; f.Ho = Ho; f.Wo = T;
+          f.s0 = src2d(x, mc, 1, 1, stride, 1, 0, 0);
+          f.ldo = mc;
+          Builder::ConvIO ios; ios.s0 = x.buf; ios.out = scb.buf;
+          b.conv(p + ".shortcut", f, *csc, ios);
+        }
+        b.macs_per_utt += macs1;
         ConvDesc e;
         e.nimg = B; e.Ho = Ho; e.Wo = T;
         e.s0 = src2d(y1, mc, 3, 3, 1, 1, 1, 1);
         Builder::ConvIO io2; io2.s0 = y1.buf; io2.out = out.buf; io2.rowlen = LENS;
-        if (sc) {
-          e.s1 = src2d(x, mc, 1, 1, stride, 1, 0, 0);
-          io2.s1 = x.buf;
-        } else {
-          e.ldr = x.ld;
-          io2.res = x.buf;
-        }
+        const A4& resid = sc ? scb : x;
+        e.ldr = resid.ld;
+        io2.res = resid.buf;
         e.ldo = mc; e.act = ACT_RELU;
         b.conv(p + ".conv2", e, c2, io2);
       }

@@ -149,12 +149,6 @@ int conv_tile_blocks(const ConvDesc& d);
 bool halo_conv_supported(const ConvDesc& d);
 hipError_t launch_conv3x3_halo(const ConvDesc& d, hipStream_t s);
 std::string halo_kernel_name(const ConvDesc& d);
-// LDS-DMA ring fp16x3 implicit GEMM for the plain large layers (conv_gemm_ring.hip);
-// launch_conv routes to it
-bool ring_supported(const ConvDesc& d);
-hipError_t launch_ring(const ConvDesc& d, hipStream_t s);
-std::string ring_kernel_name(const ConvDesc& d);
-int ring_tile_blocks(const ConvDesc& d);
 hipError_t launch_splitk_reduce(const ConvDesc& d, hipStream_t s);   // conv_gemm.hip
 // persistent short-K 1x1 GEMM (pw_gemm.hip); launch_conv routes to it
 bool pw_supported(const ConvDesc& d);

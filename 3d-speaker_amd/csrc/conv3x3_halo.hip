@@ -406,12 +406,7 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
         if (ADD) v += pb[r];
         const int q = qq, p = idx / C::QP;
         f16x4 h, l;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const _Float16 x = (_Float16)v[e];
-          h[e] = x;
-          l[e] = (_Float16)((v[e] - (float)x) * 2048.0f);
-        }
+        split_x3(v, h, l);
         *reinterpret_cast<f16x4*>(hh + p * C::ROW + 4 * q) = h;
         *reinterpret_cast<f16x4*>(hlo + p * C::ROW + 4 * q) = l;
       }

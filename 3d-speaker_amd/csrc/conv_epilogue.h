@@ -22,8 +22,31 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 // lo = fp16((v - hi) * 2^11), with packed round-toward-zero conversions (two values per
 // instruction, already packed; |v - hi| < ulp(hi) and lo keeps the remainder to 2^-22).
 typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
+#ifndef SPK_SPLIT_MIX
+#define SPK_SPLIT_MIX 1   // 0: the round-3 form (cvt back to fp32, subtract, scale, cvt: 4 VALU per value)
+#endif
+// lo of two values from their packed hi: fp16(2^11 v - 2^11 hi) by v_fma_mix{lo,hi}_f16 (the
+// hi operand read as fp16 from its packed half, 2^11 v exact), one rounding (to nearest) of an
+// exact remainder: 2.5 VALU per value with the hi conversion.  Inline asm: hipcc otherwise
+// unpacks hi and rebuilds the remainder in fp32.
+__device__ __forceinline__ uint32_t split_lo2(uint32_t hp, float v0, float v1) {
+  uint32_t r;
+  const float m = -2048.0f;
+  asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %1, %2, %4 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(r)
+      : "v"(hp), "s"(m), "v"(v0 * 2048.0f), "v"(v1 * 2048.0f));
+  return r;
+}
 __device__ __forceinline__ void split_x3(const f32x4 v, h16x4& h, h16x4& l) {
   typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+#if SPK_SPLIT_MIX
+  const uint32_t h01 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(v[0], v[1]));
+  const uint32_t h23 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(v[2], v[3]));
+  typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+  h = __builtin_bit_cast(h16x4, u32x2v{h01, h23});
+  l = __builtin_bit_cast(h16x4, u32x2v{split_lo2(h01, v[0], v[1]), split_lo2(h23, v[2], v[3])});
+#else
   const h16x2 h01 = __builtin_bit_cast(h16x2, __builtin_amdgcn_cvt_pkrtz(v[0], v[1]));
   const h16x2 h23 = __builtin_bit_cast(h16x2, __builtin_amdgcn_cvt_pkrtz(v[2], v[3]));
   const h16x2 l01 = __builtin_bit_cast(
@@ -32,6 +55,7 @@ __device__ __forceinline__ void split_x3(const f32x4 v, h16x4& h, h16x4& l) {
       h16x2, __builtin_amdgcn_cvt_pkrtz((v[2] - (float)h23[0]) * 2048.0f, (v[3] - (float)h23[1]) * 2048.0f));
   h = h16x4{h01[0], h01[1], h23[0], h23[1]};
   l = h16x4{l01[0], l01[1], l23[0], l23[1]};
+#endif
 }
 
 // Output store of the fused blocks' conv3 (res2block*.hip).  SPK_NT_STORE=1 (experiment

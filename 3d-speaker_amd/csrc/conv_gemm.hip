@@ -527,7 +527,6 @@ hipError_t launch_bk(const ConvDesc& d, const Cfg& c, hipStream_t s) {
 std::string conv_kernel_name(const ConvDesc& d) {
   if (halo_conv_supported(d)) return halo_kernel_name(d);
   if (use_x3() && pw_supported(d)) return pw_kernel_name(d);
-  if (ring_supported(d)) return ring_kernel_name(d);
   const Cfg c = select_cfg(d);
   const bool s1 = d.s1.p != nullptr || d.s1.cin > 0, add = d.s0.p2 != nullptr || d.s0.ld2 > 0;
   const bool pre = d.s0.pre_scale != nullptr;
@@ -544,7 +543,6 @@ std::string conv_kernel_name(const ConvDesc& d) {
 
 int conv_tile_blocks(const ConvDesc& d) {
   const int M = d.nimg * d.Ho * d.Wo;
-  if (ring_supported(d)) return ring_tile_blocks(d);
   const Cfg c = select_cfg(d);
   return ((M + c.bm - 1) / c.bm) * ((d.N + c.bn - 1) / c.bn);
 }
@@ -562,7 +560,6 @@ hipError_t launch_conv(const ConvDesc& dd, hipStream_t s) {
     return hipErrorInvalidValue;
   if (halo_conv_supported(d)) return launch_conv3x3_halo(d, s);
   if (use_x3() && pw_supported(d)) return launch_pw(d, s);
-  if (ring_supported(d)) return launch_ring(d, s);
   const Cfg c = select_cfg(d);
   return c.bk == 32 ? launch_bk<32>(d, c, s) : launch_bk<16>(d, c, s);
 }

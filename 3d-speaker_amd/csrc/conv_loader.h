@@ -282,16 +282,6 @@ struct BufALoader {
     }
   }
 
-  // LDS-DMA form (conv_gemm_ring.hip): this thread's byte offset of each row for the current
-  // K-tile (BUF_OOB where the operand is padding / past M / past K), then advance (tap, c)
-  __device__ __forceinline__ void offsets(const ConvDesc& d, uint32_t (&o)[AROWS]) {
-    static_assert(!S1 && !ADD && !PRE, "plain operand only");
-    const uint32_t toff = (uint32_t)(tdp * d.s0.ld + c) * 4u;
-#pragma unroll
-    for (int r = 0; r < AROWS; ++r) o[r] = ((rmask[r] >> t) & 1u) ? roff[r] + toff : BUF_OOB;
-    advance(d);
-  }
-
   __device__ __forceinline__ f32x4 value(const Slot& s, int r) const {
     f32x4 v = s.v[r];
     if (ADD || S1) v += s.v2[r];

@@ -107,13 +107,7 @@ pw_gemm_x3_kernel(const ConvDesc d) {
       const int row = idx / C::QR, q = idx % C::QR;
       const bool kin = 4 * q < K;                          // K padding columns are zero
       f16x4 h, l;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float x = kin ? v[i][e] : 0.f;
-        const _Float16 xh = (_Float16)x;
-        h[e] = xh;
-        l[e] = (_Float16)((x - (float)xh) * 2048.0f);
-      }
+      split_x3(kin ? v[i] : f32x4{0.f, 0.f, 0.f, 0.f}, h, l);
       *reinterpret_cast<f16x4*>(Ah + row * C::LROW + 4 * q) = h;
       *reinterpret_cast<f16x4*>(Al + row * C::LROW + 4 * q) = l;
     }

@@ -10,7 +10,7 @@ echo "== goldens $(date +%T)"
 timeout -k 10 420 python -u -m pytest tests/test_gpu_models.py tests/test_gpu_c2_full.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pt_models.log 2>&1
 rc=$?; tail -3 gpurun_out/pt_models.log; echo "goldens rc=$rc"
 [ $rc -ne 0 ] && exit $rc
-LIBS="3d-speaker_amd/lib/libspk_hip.so:SPK_RING=1 3d-speaker_amd/lib/libspk_hip.so" REPS=${REPS:-1} ARCHS=${ARCHS:-"eres2netv2"} bash tools/gpu_ab.sh || exit $?
+LIBS=${LIBS:-"3d-speaker_amd/lib/libspk_hip.so"} REPS=${REPS:-1} ARCHS=${ARCHS:-"eres2netv2"} bash tools/gpu_ab.sh || exit $?
 [ "${QUICK:-0}" = "1" ] && exit 0
 echo "== smoke $(date +%T)"
 timeout -k 10 400 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
