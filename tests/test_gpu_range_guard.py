@@ -58,7 +58,8 @@ def test_out_of_range_activations_take_exact_path(arch, key, factor):
     _hip._check(_hip.lib().spk_model_forward_timed(h.handle, x.data_ptr(), B, T, ws.data_ptr(), ws.numel(),
                                                    raw.data_ptr(), _hip._stream(dev), ms, 512), 'timed')
     torch.cuda.synchronize()
-    assert helpers.rel_err(raw.cpu().numpy(), ref).max() > 1e-3
+    split_only = raw.cpu().numpy()   # saturated, or non-finite (an operand past fp16's range splits to inf)
+    assert not np.isfinite(split_only).all() or helpers.rel_err(split_only, ref).max() > 1e-3
 
 
 def test_in_range_model_stays_on_split_path():
