@@ -311,13 +311,16 @@ conv3x3_halo_persistent_kernel(const ConvDesc d) {
 // output tiles over the other half of each tap's 16-deep k-steps; its partial sums meet
 // the first group's in LDS before the epilogue (two waves per SIMD, half the MFMA chain
 // per wave, halo staging spread over twice the threads).
-template <int CIN, int PIX, int KS>
+// SH = 2: frequency (row) stride 2 (CAM++ FCM: the stride-(2, 1) 3x3 convs); an output
+// tile of TH rows then reads 2 TH + 1 input rows.
+template <int CIN, int PIX, int KS, int SH = 1>
 struct HaloX3Cfg {
   static constexpr int NP = 32, NW = PIX / 32, NT = 64 * NW * KS;
   static constexpr int CINP = (CIN + 15) / 16 * 16, ROW = CINP + 8, QP = CINP / 4, Q = CIN / 4;
   static constexpr int KSTEPS = CINP / 16, KSG = KSTEPS / KS;       // k-steps per tap / per group
   static_assert(KSTEPS % KS == 0, "k-steps must split evenly over the groups");
-  static constexpr int HALO_PIX = PIX == 256 ? 340 : 204;          // (TH+2)(TW+2), TW in {8, 16, 32}
+  // max over TW in {8, 16, 32} of (SH (TH - 1) + 3)(TW + 2)
+  static constexpr int HALO_PIX = SH == 1 ? (PIX == 256 ? 340 : 204) : (PIX == 256 ? 594 : 330);
   static constexpr int HALO_F = HALO_PIX * ROW;                     // floats = hi + lo halves
   static constexpr int WRES_F = 9 * NP * ROW;                       // floats = hi + lo halves
   static constexpr int EPI = NW * 1024 * KS;                        // epilogue slabs + partner sums
@@ -327,13 +330,15 @@ struct HaloX3Cfg {
 
 // two k-groups where a tap has four k-steps (52 / 64 channels: -8 % per launch on
 // ERes2NetV2 layer2); with two k-steps (28 / 32) measured neutral to +1 %, so one group
-constexpr int halo_ks(int cin) { return cin > 32 ? 2 : 1; }
+constexpr int halo_ks(int cin, int sh = 1) { return cin > 32 || sh == 2 ? 2 : 1; }
+// (the frequency-strided form holds a 1.5x taller halo: one block per CU, so it takes the
+// second k-group too, for two waves per SIMD)
 
-template <int CIN, int TW, bool ADD, int PIX, int KS, bool PLAIN>
+template <int CIN, int TW, bool ADD, int PIX, int KS, bool PLAIN, int SH>
 __global__ void __launch_bounds__(64 * (PIX / 32) * KS, 1)
 conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
   SPK_GATE(d.run_if);
-  using C = HaloX3Cfg<CIN, PIX, KS>;
+  using C = HaloX3Cfg<CIN, PIX, KS, SH>;
   typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
   typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) float lds[C::LDS];
@@ -344,9 +349,11 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
-  constexpr int TH = PIX / TW, HW = TW + 2, HH = TH + 2;
+  constexpr int TH = PIX / TW, HW = TW + 2, HH = SH * (TH - 1) + 3;
   constexpr int hq = HH * HW * C::QP;
-  const int H = d.Ho, W = d.Wo;
+  static_assert(HH * HW <= C::HALO_PIX, "halo buffer");
+  const int H = d.Ho, W = d.Wo;                     // output
+  const int Hin = d.s0.H, Win = d.s0.W;             // input (SH = 1: the same)
   const int ntx = (W + TW - 1) / TW, nty = (H + TH - 1) / TH;
   const int ntiles = d.nimg * ntx * nty;
   // channel slice: blocks b and b+8 (one XCD) share tiles, one per 32-channel slice
@@ -371,19 +378,19 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
     const int p = idx / C::QP;
     hrc[r] = (idx < hq && qq < C::Q) ? ((uint32_t)(p / HW) << 16) | (uint32_t)(p % HW) : 0x7FFF0000u;
   }
-  const size_t img_px = (size_t)H * W;
+  const size_t img_px = (size_t)Hin * Win;
   f32x4 pa[C::PF], pb[ADD ? C::PF : 1];
   auto pf_load = [&](int t) {
     const int img = t / (ntx * nty), ty = (t / ntx) % nty, tx = t % ntx;
-    const int y0 = ty * TH - 1, x0 = tx * TW - 1;
+    const int y0 = ty * TH * SH - 1, x0 = tx * TW - 1;
     const __amdgpu_buffer_rsrc_t r0 = make_rsrc(d.s0.p + img * img_px * d.s0.ld);
     __amdgpu_buffer_rsrc_t r2;
     if (ADD) r2 = make_rsrc(d.s0.p2 + img * img_px * d.s0.ld2);
 #pragma unroll
     for (int r = 0; r < C::PF; ++r) {
       const int gy = y0 + (int)(hrc[r] >> 16), gx = x0 + (int)(hrc[r] & 0xFFFFu);
-      const bool ok = ((unsigned)gy < (unsigned)H) & ((unsigned)gx < (unsigned)W);
-      const uint32_t pix = (uint32_t)(gy * W + gx);
+      const bool ok = ((unsigned)gy < (unsigned)Hin) & ((unsigned)gx < (unsigned)Win);
+      const uint32_t pix = (uint32_t)(gy * Win + gx);
       // offsets materialised in registers before the loads (the empty asm keeps the
       // compiler from turning the select into a branch around the load: a load on only
       // some paths leaves its wait count unknown, and every later wait becomes vmcnt(0))
@@ -442,7 +449,7 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
 
   const int kg = wave / C::NW, pw = wave % C::NW;                  // k-group, pixel wave
   const int p_own = pw * 32 + li;
-  const int abase = ((p_own / TW) * HW + (p_own % TW)) * C::ROW + 8 * lh + 16 * C::KSG * kg;
+  const int abase = ((p_own / TW) * SH * HW + (p_own % TW)) * C::ROW + 8 * lh + 16 * C::KSG * kg;
   const int bbase = li * C::ROW + 8 * lh + 16 * C::KSG * kg;
   for (; t < ntiles; t += tstride) {
     const int tn = t + tstride;
@@ -520,10 +527,10 @@ int resident_blocks(K kernel, int threads) {
   return n;
 }
 
-template <int CIN, int TW, int PIX, bool ADD, bool PLAIN>
+template <int CIN, int TW, int PIX, bool ADD, bool PLAIN, int SH = 1>
 hipError_t launch_halo_x3_k(const ConvDesc& d, int nsplit, int tiles, hipStream_t s) {
-  constexpr int NT = HaloX3Cfg<CIN, PIX, halo_ks(CIN)>::NT;
-  auto k = conv3x3_halo_x3_kernel<CIN, TW, ADD, PIX, halo_ks(CIN), PLAIN>;
+  constexpr int NT = HaloX3Cfg<CIN, PIX, halo_ks(CIN, SH), SH>::NT;
+  auto k = conv3x3_halo_x3_kernel<CIN, TW, ADD, PIX, halo_ks(CIN, SH), PLAIN, SH>;
   static const int per_cu = resident_blocks(k, NT);
   // nsplit blocks per tile group of 8; a multiple of 8 * nsplit (or everything when small)
   const int slots = per_cu * device_cus();
@@ -541,6 +548,11 @@ hipError_t launch_halo_x3_tw(const ConvDesc& d, hipStream_t s) {
   const int nsplit = (d.N + 31) / 32;
   const bool plain = !d.res && !d.post_scale && !d.rowlen && !d.osplit &&
                      ((double)d.nimg * d.Ho * d.Wo * d.ldo + d.N) * 4.0 < 0x7FFFFFF0;
+  if constexpr (CIN == 32) {   // CAM++ FCM: frequency-strided 3x3 (halo_conv_supported)
+    if (d.s0.sh == 2)
+      return plain ? launch_halo_x3_k<CIN, TW, PIX, false, true, 2>(d, nsplit, tiles, s)
+                   : launch_halo_x3_k<CIN, TW, PIX, false, false, 2>(d, nsplit, tiles, s);
+  }
   if (d.s0.p2)
     return plain ? launch_halo_x3_k<CIN, TW, PIX, true, true>(d, nsplit, tiles, s)
                  : launch_halo_x3_k<CIN, TW, PIX, true, false>(d, nsplit, tiles, s);
@@ -639,9 +651,13 @@ bool halo_conv_supported(const ConvDesc& d) {
   const ConvSrc& s = d.s0;
   if (off == 1 || (off > 1 && off == s.cin)) return false;
   if (s.vlen) return false;   // masked (pre-activated) inputs take the implicit GEMM
-  return !d.kcb && s.kh == 3 && s.kw == 3 && s.sh == 1 && s.sw == 1 && s.ph == 1 && s.pw == 1 && s.dh == 1 && s.dw == 1 &&
+  // frequency stride 2: the x3 kernel's SH = 2 form, 32 input channels (CAM++ FCM)
+  const bool geom = s.sh == 1 ? (d.Ho == s.H && d.Wo == s.W)
+                              : (s.sh == 2 && s.cin == 32 && !s.p2 && s.ld2 == 0 && x3_halo_ok(d) &&
+                                 d.Ho == (s.H - 1) / 2 + 1 && d.Wo == s.W);
+  return !d.kcb && s.kh == 3 && s.kw == 3 && s.sw == 1 && s.ph == 1 && s.pw == 1 && s.dh == 1 && s.dw == 1 &&
          !s.reflect && !s.pre_scale && !d.s1.p && d.s1.cin == 0 && d.ksplit == 1 && d.N <= 64 &&
-         (s.cin == 28 || s.cin == 32 || s.cin == 52 || s.cin == 64) && d.Ho == s.H && d.Wo == s.W &&
+         (s.cin == 28 || s.cin == 32 || s.cin == 52 || s.cin == 64) && geom &&
          d.Kp >= 9 * s.cin && s.ld % 4 == 0 && (!s.p2 || s.ld2 % 4 == 0) &&
          // the x3 kernel addresses one image through a buffer resource (32-bit offsets)
          (double)s.H * s.W * std::max(s.ld, s.p2 ? s.ld2 : 0) * 4.0 < 0x7FFFFFF0 - 64;
@@ -655,9 +671,10 @@ std::string halo_kernel_name(const ConvDesc& d) {
   if (x3_halo_ok(d)) {
     const int px = 128;
     return "conv3x3_halo_x3_kernel<" + std::to_string(d.s0.cin) + ", " + std::to_string(pick_tw(d.Ho, d.Wo, px)) +
-           ", " + (add ? "true" : "false") + ", " + std::to_string(px) + ", " + std::to_string(halo_ks(d.s0.cin)) + ", " +
+           ", " + (add ? "true" : "false") + ", " + std::to_string(px) + ", " + std::to_string(halo_ks(d.s0.cin, d.s0.sh)) + ", " +
            ((!d.res && d.ldr == 0 && !d.post_scale && !d.rowlen && !d.osplit &&
-             ((double)d.nimg * d.Ho * d.Wo * d.ldo + d.N) * 4.0 < 0x7FFFFFF0) ? "true" : "false") + ">";
+             ((double)d.nimg * d.Ho * d.Wo * d.ldo + d.N) * 4.0 < 0x7FFFFFF0) ? "true" : "false") + ", " +
+           std::to_string(d.s0.sh) + ">";
   }
   if (persistent_ok(d))
     return "conv3x3_halo_persistent_kernel<" + std::to_string(d.s0.cin) + ", " + std::to_string(tw) + ", " +

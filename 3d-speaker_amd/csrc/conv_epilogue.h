@@ -113,10 +113,16 @@ __device__ __forceinline__ float epilogue_elem(const ConvDesc& d, int m, int n, 
 // layer never takes) forces waits for everything issued before it (vmcnt counts in order).
 // WIDE = true lets a wave with four accumulator tiles (the LDS-DMA GEMM's 32 x 128) take the
 // one-round-trip paths too (16 residual / AFF quads in flight).
-template <int TM, int TN, bool LEAN = false, bool PLAIN = false, bool WIDE = false, class RowMap>
+// `hook` (persistent GEMM): called once the epilogue's own global loads are all issued (fast
+// paths) or done (the others), so loads it issues -- the next tile's first K-tiles -- are in
+// flight during the epilogue without delaying its waits (vmcnt retires loads in order).
+struct NoHook {
+  __device__ void operator()() const {}
+};
+template <int TM, int TN, bool LEAN = false, bool PLAIN = false, bool WIDE = false, class RowMap, class Hook = NoHook>
 __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f32x16 (&acc)[TM][TN], int wave,
                                                int lane, int nwave, int M, RowMap rowmap,
-                                               const f32x4* pre_bias = nullptr) {
+                                               const f32x4* pre_bias = nullptr, Hook hook = Hook{}) {
   const int li = lane & 31, lh = lane >> 5;
   // one 32x32 accumulator tile at a time through a per-wave LDS slab:
   // registers -> LDS in the MFMA C layout (col = lane&31, row = (r&3)+8(r>>2)+4(lane>>5)),
@@ -144,7 +150,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
   if constexpr (NTL <= 2 || (WIDE && NTL <= 4)) {
     if (LEAN || PLAIN || (vec && !part && !d.affx && !d.gate && !d.rowbias)) {
       const int c4 = (lane & 7) * 4;
-      f32x4 ra4[NTL][4];
+      f32x4 ra4[NTL][4], bias4[NTL], ps4[NTL], pt4[NTL];
 #pragma unroll
       for (int tile = 0; tile < NTL; ++tile) {
         const int i = tile / TN, j = tile % TN;
@@ -157,7 +163,21 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
             ra4[tile][q] = *reinterpret_cast<const f32x4*>(d.res + (size_t)m * d.ldr + n);
           }
         }
+        // per-channel operands requested with the residual: one round trip for all of them
+        bias4[tile] = f32x4{0.f, 0.f, 0.f, 0.f};
+        ps4[tile] = f32x4{1.f, 1.f, 1.f, 1.f};
+        pt4[tile] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (!PLAIN) {
+          const int nn = n < d.N ? n : 0;
+          if (pre_bias) bias4[tile] = pre_bias[tile];
+          else if (d.bias) bias4[tile] = *reinterpret_cast<const f32x4*>(d.bias + nn);
+          if (d.post_scale) {
+            ps4[tile] = *reinterpret_cast<const f32x4*>(d.post_scale + nn);
+            pt4[tile] = *reinterpret_cast<const f32x4*>(d.post_shift + nn);
+          }
+        }
       }
+      hook();
 #pragma unroll
       for (int tile = 0; tile < NTL; ++tile) {
         const int i = tile / TN, j = tile % TN;
@@ -192,13 +212,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
         }
         if (n >= d.N) continue;
         float* const ocol = out_at(d, 0, n);   // plane / column split once per tile, not per row
-        f32x4 bias = {0.f, 0.f, 0.f, 0.f}, ps = {1.f, 1.f, 1.f, 1.f}, pt = {0.f, 0.f, 0.f, 0.f};
-        if (pre_bias) bias = pre_bias[tile];
-        else if (d.bias) bias = *reinterpret_cast<const f32x4*>(d.bias + n);
-        if (!PLAIN && d.post_scale) {
-          ps = *reinterpret_cast<const f32x4*>(d.post_scale + n);
-          pt = *reinterpret_cast<const f32x4*>(d.post_shift + n);
-        }
+        const f32x4 bias = bias4[tile], ps = ps4[tile], pt = pt4[tile];
         const float* ct = cw + tile * 1024;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -240,6 +254,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
           }
         }
       }
+      hook();   // (its bias loads below then wait for the hook's loads: no persistent grid here)
 #pragma unroll
       for (int tile = 0; tile < NTL; ++tile) {
         const int i = tile / TN, j = tile % TN;
@@ -289,7 +304,10 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
       return;
     }
   }
-  if constexpr (LEAN || PLAIN) return;
+  if constexpr (LEAN || PLAIN) {
+    hook();
+    return;
+  }
 #pragma unroll 1
   for (int tile = 0; tile < TM * TN; ++tile) {
     {
@@ -381,6 +399,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
       }
     }
   }
+  hook();   // the general path: its loads are all done
   range_note(d.range_flag, amax);
 }
 

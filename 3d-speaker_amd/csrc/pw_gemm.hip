@@ -71,6 +71,10 @@ pw_gemm_x3_kernel(const ConvDesc d) {
   const int mt0 = bid / nN;
   const int K0 = d.s0.cin;                                 // s0 channels, then s1 (S1)
   const int K = d.K;
+  // strided 1x1 (CAM++ FCM projection shortcut, frequency stride 2): output pixel m reads
+  // input pixel (img, ho * sh, wo * sw); the s0 address of a row is re-derived from m
+  const bool strided = d.s0.sh != 1 || d.s0.sw != 1;
+  const int HoWo = d.Ho * d.Wo;
 
   // ---- weights of the N-slice -> LDS (once)
   for (int idx = tid; idx < BN * (KP / 8); idx += C::NT) {
@@ -93,10 +97,15 @@ pw_gemm_x3_kernel(const ConvDesc d) {
       const int row = idx / C::QR, q = idx % C::QR;
       int m = mt * C::BM + row;
       m = m < M ? m : M - 1;
+      int m0r = m;                                         // s0 row of output pixel m
+      if (strided) {
+        const int img = m / HoWo, rem = m - img * HoWo, ho = rem / d.Wo, wo = rem - ho * d.Wo;
+        m0r = (img * d.s0.H + ho * d.s0.sh) * d.s0.W + wo * d.s0.sw;
+      }
       const int k = 4 * q;
       const float* src;
       if (S1 && k >= K0) src = d.s1.p + (size_t)m * d.s1.ld + min(k - K0, d.s1.cin - 4);
-      else src = d.s0.p + (size_t)m * d.s0.ld + min(k, K0 - 4);
+      else src = d.s0.p + (size_t)m0r * d.s0.ld + min(k, K0 - 4);
       v[i] = *reinterpret_cast<const f32x4*>(src);
     }
   };
@@ -224,7 +233,7 @@ hipError_t launch_pw_t(const ConvDesc& d, hipStream_t s) {
   return hipGetLastError();
 }
 
-int pw_bn(const ConvDesc& d) { return d.N <= 64 ? 64 : 128; }
+int pw_bn(const ConvDesc& d) { return d.N <= 32 ? 32 : d.N <= 64 ? 64 : 128; }
 
 }  // namespace
 
@@ -236,10 +245,14 @@ bool pw_supported(const ConvDesc& d) {
                          ? true
                          : (d.s1.kh == 1 && d.s1.kw == 1 && d.s1.sh == 1 && d.s1.sw == 1 && d.s1.ph == 0 &&
                             d.s1.pw == 0 && d.s1.cin % 4 == 0 && d.s1.ld % 4 == 0);
-  return d.wh && d.wl && !a.vlen && a.kh == 1 && a.kw == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0 && !a.reflect &&
-         !a.pre_scale && !a.p2 && a.ld2 == 0 && s1_ok && (d.Kp == 64 || d.Kp == 128) && d.N <= 256 &&
-         d.N % 4 == 0 && !d.affx && !d.gate && !d.rowbias && !d.rowlen && d.ksplit == 1 && a.cin % 4 == 0 &&
-         a.H == d.Ho && a.W == d.Wo && d.nimg * d.Ho * d.Wo >= 65536;
+  // stride: output rows map onto every sh-th / sw-th input row (pad 0); the K-concatenated
+  // s1 operand keeps the output geometry
+  const bool geom = a.sh >= 1 && a.sw >= 1 && (a.H - 1) / a.sh + 1 == d.Ho && (a.W - 1) / a.sw + 1 == d.Wo &&
+                    ((a.sh == 1 && a.sw == 1) || (!d.s1.p && d.s1.cin == 0));
+  return d.wh && d.wl && !a.vlen && a.kh == 1 && a.kw == 1 && geom && a.ph == 0 && a.pw == 0 && !a.reflect &&
+         !a.pre_scale && !a.p2 && a.ld2 == 0 && s1_ok && (d.Kp == 32 || d.Kp == 64 || d.Kp == 128) && d.N <= 256 &&
+         (d.Kp != 32 || d.N <= 32) && d.N % 4 == 0 && !d.affx && !d.gate && !d.rowbias && !d.rowlen && d.ksplit == 1 &&
+         a.cin % 4 == 0 && d.nimg * d.Ho * d.Wo >= 65536;
 }
 
 std::string pw_kernel_name(const ConvDesc& d) {
@@ -257,6 +270,7 @@ hipError_t launch_pw(const ConvDesc& d, hipStream_t s) {
   if (d.Kp == KP && bn == BNV)                                                  \
     return s1 ? (d.res ? launch_pw_t<KP, BNV, true, true>(d, s) : launch_pw_t<KP, BNV, true, false>(d, s)) \
               : (d.res ? launch_pw_t<KP, BNV, false, true>(d, s) : launch_pw_t<KP, BNV, false, false>(d, s));
+  SPK_PW(32, 32)
   SPK_PW(64, 64)
   SPK_PW(64, 128)
   SPK_PW(128, 64)
