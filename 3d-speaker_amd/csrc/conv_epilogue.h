@@ -1,5 +1,7 @@
 // Fused conv epilogue shared by the implicit-GEMM and the halo-tiled conv kernels.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace spk {
@@ -16,6 +18,13 @@ __device__ __forceinline__ float apply_act(float v, int act) {
     case ACT_TANH: return tanhf(v);
     default: return v;
   }
+}
+
+// AFF combine (fusion.py:26-28): x (1 + tanh v) + y (1 - tanh v) = 2 (y + sigmoid(2 v) (x - y))
+// -- one exp and one reciprocal instead of tanhf's branches (aff.hip uses the same form)
+__device__ __forceinline__ float aff_combine(float v, float x, float y) {
+  const float sg = __frcp_rn(1.0f + __expf(-2.0f * v));
+  return 2.0f * fmaf(sg, x - y, y);
 }
 
 // fp16x3 split of a staged fp32 quad (conv_gemm.hip "fp16x3"): hi = fp16(v) and
@@ -83,7 +92,7 @@ __device__ __forceinline__ float epilogue_elem(const ConvDesc& d, int m, int n, 
   if (d.rowbias) v += d.rowbias[(size_t)(m / (d.Ho * d.Wo)) * d.rowbias_ld + n];
   if (d.res) v += d.res[(size_t)m * d.ldr + n];
   if (d.affx) {
-    const float t = 1.0f + tanhf(v);
+    const float t = 1.0f + tanhf(v);   // (scalar fallback: split-K reduce)
     return d.affx[(size_t)m * d.ldx + n] * t + d.affy[(size_t)m * d.ldy + n] * (2.0f - t);
   }
   v = apply_act(v, d.act);
@@ -192,14 +201,24 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
           float* const ocol = d.out + n;
           f32x4 o[4];
           int mq[4];
+          // the layer's activation resolved once per tile (compile-time forms for the common ones)
+          auto act_rows = [&](auto actc) {
+            constexpr int A = decltype(actc)::value;   // -1: general
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int rl = q * 8 + (lane >> 3);
-            mq[q] = rowmap(i * 32 + rl);
-            o[q] = *reinterpret_cast<const f32x4*>(ct + rl * 32 + c4) + bias;
+            for (int q = 0; q < 4; ++q) {
+              const int rl = q * 8 + (lane >> 3);
+              mq[q] = rowmap(i * 32 + rl);
+              o[q] = *reinterpret_cast<const f32x4*>(ct + rl * 32 + c4) + bias;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[q][e] = apply_act(apply_act(o[q][e], d.act), d.act2);
-          }
+              for (int e = 0; e < 4; ++e) {
+                if constexpr (A >= 0) o[q][e] = apply_act(o[q][e], A);
+                else o[q][e] = apply_act(apply_act(o[q][e], d.act), d.act2);
+              }
+            }
+          };
+          if (d.act2 == ACT_NONE && d.act == ACT_HTANH) act_rows(std::integral_constant<int, ACT_HTANH>{});
+          else if (d.act2 == ACT_NONE && d.act == ACT_RELU) act_rows(std::integral_constant<int, ACT_RELU>{});
+          else act_rows(std::integral_constant<int, -1>{});
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const bool ok = n < d.N && mq[q] >= 0 && mq[q] < M;
@@ -214,22 +233,39 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
         float* const ocol = out_at(d, 0, n);   // plane / column split once per tile, not per row
         const f32x4 bias = bias4[tile], ps = ps4[tile], pt = pt4[tile];
         const float* ct = cw + tile * 1024;
+        // the rows of a tile with the layer's activation resolved once (not per element): the
+        // common forms (one activation, no post-affine, no ragged mask) as compile-time
+        // variants, everything else through the general form
+        auto rows = [&](auto actc) {
+          constexpr int A = decltype(actc)::value;   // -1: general
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int rl = q * 8 + (lane >> 3);
-          const int m = rowmap(i * 32 + rl);
-          if (m < 0 || m >= M) continue;
-          f32x4 o = *reinterpret_cast<const f32x4*>(ct + rl * 32 + c4) + bias + ra4[tile][q];
+          for (int q = 0; q < 4; ++q) {
+            const int rl = q * 8 + (lane >> 3);
+            const int m = rowmap(i * 32 + rl);
+            if (m < 0 || m >= M) continue;
+            f32x4 o = *reinterpret_cast<const f32x4*>(ct + rl * 32 + c4) + bias + ra4[tile][q];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float x = apply_act(o[e], d.act);
-            if (!PLAIN && d.post_scale) x = x * ps[e] + pt[e];
-            o[e] = apply_act(x, d.act2);
+            for (int e = 0; e < 4; ++e) {
+              if constexpr (A >= 0) {
+                o[e] = apply_act(o[e], A);
+              } else {
+                float x = apply_act(o[e], d.act);
+                if (!PLAIN && d.post_scale) x = x * ps[e] + pt[e];
+                o[e] = apply_act(x, d.act2);
+              }
+            }
+            if constexpr (A < 0) {
+              if (!PLAIN && row_masked(d, m)) o = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+            *reinterpret_cast<f32x4*>(ocol + (size_t)m * d.ldo) = o;
           }
-          if (!PLAIN && row_masked(d, m)) o = f32x4{0.f, 0.f, 0.f, 0.f};
-          amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
-          *reinterpret_cast<f32x4*>(ocol + (size_t)m * d.ldo) = o;
-        }
+        };
+        const bool simple = !d.post_scale && d.act2 == ACT_NONE && !d.rowlen;
+        if (simple && d.act == ACT_HTANH) rows(std::integral_constant<int, ACT_HTANH>{});
+        else if (simple && d.act == ACT_RELU) rows(std::integral_constant<int, ACT_RELU>{});
+        else if (simple && d.act == ACT_NONE) rows(std::integral_constant<int, ACT_NONE>{});
+        else rows(std::integral_constant<int, -1>{});
       }
       range_note(d.range_flag, amax);
       return;
@@ -292,8 +328,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
           f32x4 o = *reinterpret_cast<const f32x4*>(ct + rl * 32 + c4) + bias;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float t = 1.0f + tanhf(o[e]);
-            o[e] = xa[tile][q][e] * t + ya[tile][q][e] * (2.0f - t);
+            o[e] = aff_combine(o[e], xa[tile][q][e], ya[tile][q][e]);
           }
           if (row_masked(d, m)) o = f32x4{0.f, 0.f, 0.f, 0.f};
           amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
@@ -358,8 +393,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
             if (d.affx) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
-                const float t = 1.0f + tanhf(o[e]);
-                o[e] = xa4[q][e] * t + ya4[q][e] * (2.0f - t);
+                o[e] = aff_combine(o[e], xa4[q][e], ya4[q][e]);
               }
             } else {
 #pragma unroll

@@ -202,6 +202,10 @@ struct X3Cfg {
 template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE, bool BUF, bool X1>
 __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
   SPK_GATE(d.run_if);
+  // experiment: the two blocks that share a CU start a part of a tile apart (blocks 256..511
+  // of the first round wait), so their load / epilogue phases stop coinciding
+  if (d.stagger && blockIdx.x >= 256 && blockIdx.x < 512)
+    for (int i = 0; i < d.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   using C = X3Cfg<BM, BN, WM, WN, X1>;
   constexpr int BK = C::BK, TM = C::TM, TN = C::TN, RPP = C::RPP, AROWS = C::AROWS;
   static_assert(TM >= 1 && TN >= 1 && BM % RPP == 0, "tile shape");
@@ -552,6 +556,11 @@ bool conv_use_x3() { return use_x3(); }
 hipError_t launch_conv(const ConvDesc& dd, hipStream_t s) {
   ConvDesc d = dd;
   d.run_if = launch_gate();
+  static const int stagger = [] {
+    const char* e = std::getenv("SPK_GEMM_STAGGER");
+    return e ? std::atoi(e) : 0;
+  }();
+  d.stagger = stagger;
   // host-side shape checks: every float4 access must stay aligned and in range
   if (d.s0.cin % 4 || d.s0.ld % 4 || (d.s0.p2 && d.s0.ld2 % 4) || d.Kp % KP_ALIGN || (d.osplit ? (d.osplit % 4 || d.ldo < d.osplit) : d.ldo < d.N) ||
       (d.s1.p && (d.s1.cin % 4 || d.s1.ld % 4)) || d.N <= 0 || d.nimg <= 0 || d.Ho <= 0 || d.Wo <= 0 ||

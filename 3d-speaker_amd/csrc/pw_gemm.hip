@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #include "common.h"
 #include "conv_epilogue.h"
@@ -159,16 +160,30 @@ pw_gemm_x3_kernel(const ConvDesc d) {
     }
     if (nok) {
       float amax = 0.f;
+      // the activation resolved once per tile: compile-time forms for the common layers
+      auto rows = [&](auto actc) {
+        constexpr int A = decltype(actc)::value;   // -1: general
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mbase + (r & 3) + 8 * (r >> 2);
-        if (m >= M) continue;
-        float v = apply_act(acc[r] + accx[r] * (1.0f / 2048.0f) + bias + res[r], d.act);
-        if (d.post_scale) v = v * ps + pt;
-        v = apply_act(v, d.act2);                          // no ragged rows (pw_supported)
-        amax = fmaxf(amax, fabsf(v));
-        ocol[(size_t)m * d.ldo] = v;
-      }
+        for (int r = 0; r < 16; ++r) {
+          const int m = mbase + (r & 3) + 8 * (r >> 2);
+          if (m >= M) continue;
+          float v = acc[r] + accx[r] * (1.0f / 2048.0f) + bias + res[r];
+          if constexpr (A >= 0) {
+            v = apply_act(v, A);
+          } else {
+            v = apply_act(v, d.act);
+            if (d.post_scale) v = v * ps + pt;
+            v = apply_act(v, d.act2);                      // no ragged rows (pw_supported)
+          }
+          amax = fmaxf(amax, fabsf(v));
+          ocol[(size_t)m * d.ldo] = v;
+        }
+      };
+      const bool simple = !d.post_scale && d.act2 == ACT_NONE;
+      if (simple && d.act == ACT_HTANH) rows(std::integral_constant<int, ACT_HTANH>{});
+      else if (simple && d.act == ACT_RELU) rows(std::integral_constant<int, ACT_RELU>{});
+      else if (simple && d.act == ACT_NONE) rows(std::integral_constant<int, ACT_NONE>{});
+      else rows(std::integral_constant<int, -1>{});
       range_note(d.range_flag, amax);
     }
   };
