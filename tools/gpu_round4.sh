@@ -32,7 +32,7 @@ echo "== pmc sq $(date +%T)"
 timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmc_mfma -o run --output-format csv -- python tools/profile_steps.py --arch eres2netv2 > gpurun_out/pmc_mfma.log 2>&1
 rc=$?; echo "pmc sq rc=$rc"
 if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc_mfma.log; exit $rc; fi
-python tools/pmc_mfma.py gpurun_out/pmc_mfma -o gpurun_out/sq_counters.json | head -12
+python tools/pmc_mfma.py gpurun_out/pmc_mfma -o gpurun_out/sq_counters.json > gpurun_out/sq_counters.txt 2>&1; head -12 gpurun_out/sq_counters.txt
 echo "== rocprofv3 stats $(date +%T)"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
     python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1
