@@ -13,8 +13,8 @@ __device__ __forceinline__ float apply_act(float v, int act) {
   switch (act) {
     case ACT_RELU: return fmaxf(v, 0.0f);
     case ACT_HTANH: return fminf(fmaxf(v, 0.0f), 20.0f);
-    case ACT_SILU: return v / (1.0f + __expf(-v));
-    case ACT_SIGMOID: return 1.0f / (1.0f + __expf(-v));
+    case ACT_SILU: return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));   // v_rcp (1 ulp), no IEEE divide sequence
+    case ACT_SIGMOID: return __builtin_amdgcn_rcpf(1.0f + __expf(-v));
     case ACT_TANH: return tanhf(v);
     default: return v;
   }
@@ -23,7 +23,7 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 // AFF combine (fusion.py:26-28): x (1 + tanh v) + y (1 - tanh v) = 2 (y + sigmoid(2 v) (x - y))
 // -- one exp and one reciprocal instead of tanhf's branches (aff.hip uses the same form)
 __device__ __forceinline__ float aff_combine(float v, float x, float y) {
-  const float sg = __frcp_rn(1.0f + __expf(-2.0f * v));
+  const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * v));
   return 2.0f * fmaf(sg, x - y, y);
 }
 

@@ -180,6 +180,9 @@ conv_gemm_kernel(const ConvDesc d) {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#ifndef SPK_GEMM_WE
+#define SPK_GEMM_WE 0   // 1: write-early K loop (A/B build)
+#endif
 
 template <int BM, int BN, int WM, int WN, bool X1 = false>
 struct X3Cfg {
@@ -348,6 +351,33 @@ __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
         }
     }
   };
+#if SPK_GEMM_WE
+  // write-early schedule (cdna_hip_programming.md T14): right after each barrier the NEXT
+  // K-tile's registers go to the idle LDS buffer and the set is refilled three K-tiles ahead,
+  // so the LDS stores overlap this step's MFMAs and the barrier waits on nothing but the
+  // fragment reads.  Invariant at the top of step kt: buffer kt % 2 holds K-tile kt, set
+  // (kt+1) % 2 holds kt+1 (landed: requested two steps ago), set kt % 2 holds kt+2 (in flight).
+  if (kt0 < kt1) {
+    load_tile(kt0, set0);
+    load_tile(min(kt0 + 1, kt1 - 1), set1);
+    store_tile(0, set0);
+    load_tile(min(kt0 + 2, kt1 - 1), set0);
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; kt += 2) {
+      // even step: buffer 0 = kt, set 1 = kt+1, set 0 = kt+2
+      store_tile(1, set1);                    // past the last K-tile: the idle buffer (unread)
+      load_tile(min(kt + 3, kt1 - 1), set1);
+      compute(0);
+      __syncthreads();
+      if (kt + 1 >= kt1) break;
+      // odd step: buffer 1 = kt+1, set 0 = kt+2, set 1 = kt+3
+      store_tile(0, set0);
+      load_tile(min(kt + 4, kt1 - 1), set0);
+      compute(1);
+      __syncthreads();
+    }
+  }
+#else
   if (kt0 < kt1) {
     load_tile(kt0, set0);
     load_tile(min(kt0 + 1, kt1 - 1), set1);
@@ -383,6 +413,7 @@ __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
       __syncthreads();
     }
   }
+#endif
   if constexpr (!X1) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)

@@ -206,16 +206,21 @@ struct ERes2Builder {
   // shortcut from 128 channels, or the stage's first block with a 1x1 stride-1 projection
   // shortcut from 64; stage 2 (slices 33..64, 256 output channels) -- identity from 256, or
   // the first block: 1x1 stride-2 conv1 and projection shortcut from 128.
+  // (ERes2Net's BasicBlockERes2Net, ERes2Net.py:61-87, has the forward of ERes2NetV2's block,
+  // ERes2NetV2.py:65-91: ERes2Net-large's stage 1 -- width 32 -- takes the same kernel)
   bool fusable(const std::string& p, const T4& x, int stride, int width, int Cout, bool use_aff) const {
     const bool sc = m.has(p + ".shortcut.0.weight");
-    const bool common = v2 && !use_aff && scale == 2 && x.ld == x.C && !b.ragged && b.x3() &&
+    const bool common = !use_aff && scale == 2 && x.ld == x.C && !b.ragged && b.x3() &&
                         std::getenv("SPK_NO_BLOCK_FUSION") == nullptr;
     // stage 1 (res2block.hip): slices <= 32, 128 output channels, identity or 64 -> 128 projection
     const bool s1 = stride == 1 && width <= 32 && Cout == 128 &&
                     (sc ? (x.C == 64 && std::getenv("SPK_NO_PROJ_FUSION") == nullptr) : x.C == 128);
     // stage 2 (res2block_s2.hip): slices 33..64, 256 -> 256 identity, or 128 -> 256 at stride 2
     // with the projection shortcut
-    const bool s2 = width > 32 && width <= 64 && Cout == 256 && std::getenv("SPK_NO_S2_FUSION") == nullptr &&
+    // (ERes2Net-large's unfused stage 2 -- 64-wide slices: no padding, the two-k-group halo
+    // kernel -- measured 1.55 ms per block against 1.70 fused on MI355X: stage 2 fuses for
+    // ERes2NetV2 only)
+    const bool s2 = v2 && width > 32 && width <= 64 && Cout == 256 && std::getenv("SPK_NO_S2_FUSION") == nullptr &&
                     (sc ? (x.C == 128 && stride == 2 && std::getenv("SPK_NO_PROJ_FUSION") == nullptr)
                         : (x.C == 256 && stride == 1));
     return common && (s1 || s2);
