@@ -76,7 +76,6 @@ struct ConvDesc {
   // block, and the taps of a block follow each other, so the block's input pixels are re-read
   // from L2 within a few K-tiles instead of once per sweep over the whole K (runtime.cpp pack)
   int kcb = 0;
-  int stagger = 0;              // experiment (SPK_GEMM_STAGGER): start delay of half the first blocks
 };
 
 // fp16x3 range guard.  The split-precision GEMMs represent an operand as two fp16 values,

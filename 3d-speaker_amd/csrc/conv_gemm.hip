@@ -180,9 +180,7 @@ conv_gemm_kernel(const ConvDesc d) {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-#ifndef SPK_GEMM_WE
-#define SPK_GEMM_WE 0   // 1: write-early K loop (A/B build)
-#endif
+
 
 template <int BM, int BN, int WM, int WN, bool X1 = false>
 struct X3Cfg {
@@ -205,10 +203,6 @@ struct X3Cfg {
 template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE, bool BUF, bool X1>
 __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
   SPK_GATE(d.run_if);
-  // experiment: the two blocks that share a CU start a part of a tile apart (blocks 256..511
-  // of the first round wait), so their load / epilogue phases stop coinciding
-  if (d.stagger && blockIdx.x >= 256 && blockIdx.x < 512)
-    for (int i = 0; i < d.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   using C = X3Cfg<BM, BN, WM, WN, X1>;
   constexpr int BK = C::BK, TM = C::TM, TN = C::TN, RPP = C::RPP, AROWS = C::AROWS;
   static_assert(TM >= 1 && TN >= 1 && BM % RPP == 0, "tile shape");
@@ -351,33 +345,6 @@ __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
         }
     }
   };
-#if SPK_GEMM_WE
-  // write-early schedule (cdna_hip_programming.md T14): right after each barrier the NEXT
-  // K-tile's registers go to the idle LDS buffer and the set is refilled three K-tiles ahead,
-  // so the LDS stores overlap this step's MFMAs and the barrier waits on nothing but the
-  // fragment reads.  Invariant at the top of step kt: buffer kt % 2 holds K-tile kt, set
-  // (kt+1) % 2 holds kt+1 (landed: requested two steps ago), set kt % 2 holds kt+2 (in flight).
-  if (kt0 < kt1) {
-    load_tile(kt0, set0);
-    load_tile(min(kt0 + 1, kt1 - 1), set1);
-    store_tile(0, set0);
-    load_tile(min(kt0 + 2, kt1 - 1), set0);
-    __syncthreads();
-    for (int kt = kt0; kt < kt1; kt += 2) {
-      // even step: buffer 0 = kt, set 1 = kt+1, set 0 = kt+2
-      store_tile(1, set1);                    // past the last K-tile: the idle buffer (unread)
-      load_tile(min(kt + 3, kt1 - 1), set1);
-      compute(0);
-      __syncthreads();
-      if (kt + 1 >= kt1) break;
-      // odd step: buffer 1 = kt+1, set 0 = kt+2, set 1 = kt+3
-      store_tile(0, set0);
-      load_tile(min(kt + 4, kt1 - 1), set0);
-      compute(1);
-      __syncthreads();
-    }
-  }
-#else
   if (kt0 < kt1) {
     load_tile(kt0, set0);
     load_tile(min(kt0 + 1, kt1 - 1), set1);
@@ -395,7 +362,6 @@ __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
       // even step: LDS buffer 0 holds kt, set 1 holds kt+1 (in flight), set 0 is free
 #if SPK_GEXP != 3
       load_tile(min(kt + 2, kt1 - 1), set0);
-#endif
       compute(0);
 #if SPK_GEXP != 5
       if (UNCOND || kt + 1 < kt1) store_tile(1, set1);
@@ -587,11 +553,6 @@ bool conv_use_x3() { return use_x3(); }
 hipError_t launch_conv(const ConvDesc& dd, hipStream_t s) {
   ConvDesc d = dd;
   d.run_if = launch_gate();
-  static const int stagger = [] {
-    const char* e = std::getenv("SPK_GEMM_STAGGER");
-    return e ? std::atoi(e) : 0;
-  }();
-  d.stagger = stagger;
   // host-side shape checks: every float4 access must stay aligned and in range
   if (d.s0.cin % 4 || d.s0.ld % 4 || (d.s0.p2 && d.s0.ld2 % 4) || d.Kp % KP_ALIGN || (d.osplit ? (d.osplit % 4 || d.ldo < d.osplit) : d.ldo < d.N) ||
       (d.s1.p && (d.s1.cin % 4 || d.s1.ld % 4)) || d.N <= 0 || d.nimg <= 0 || d.Ho <= 0 || d.Wo <= 0 ||

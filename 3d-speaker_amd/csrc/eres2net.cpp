@@ -18,6 +18,7 @@
 //     applying x*(1+tanh a) + y*(1-tanh a) in its epilogue.
 #include <cmath>
 #include <cstdlib>
+#include <string>
 
 #include "aff.h"
 #include "misc.h"
@@ -217,10 +218,15 @@ struct ERes2Builder {
                     (sc ? (x.C == 64 && std::getenv("SPK_NO_PROJ_FUSION") == nullptr) : x.C == 128);
     // stage 2 (res2block_s2.hip): slices 33..64, 256 -> 256 identity, or 128 -> 256 at stride 2
     // with the projection shortcut
-    // (ERes2Net-large's unfused stage 2 -- 64-wide slices: no padding, the two-k-group halo
-    // kernel -- measured 1.55 ms per block against 1.70 fused on MI355X: stage 2 fuses for
-    // ERes2NetV2 only)
-    const bool s2 = v2 && width > 32 && width <= 64 && Cout == 256 && std::getenv("SPK_NO_S2_FUSION") == nullptr &&
+    // Stage 2 runs unfused unless SPK_S2_FUSION=1: since the round-4 epilogue work the four
+    // kernels of a block (1x1 GEMM, two halo 3x3 convs, 1x1 + residual) beat the fused kernel
+    // on MI355X -- ERes2NetV2 layer2 5.91 vs 6.77 ms, forward 24.05 vs 25.27 ms (two reps each);
+    // ERes2Net-large 1.55 vs 1.70 ms per block
+    static const bool s2_on = [] {
+      const char* e = std::getenv("SPK_S2_FUSION");
+      return e && std::string(e) == "1";
+    }();
+    const bool s2 = s2_on && width > 32 && width <= 64 && Cout == 256 &&
                     (sc ? (x.C == 128 && stride == 2 && std::getenv("SPK_NO_PROJ_FUSION") == nullptr)
                         : (x.C == 256 && stride == 1));
     return common && (s1 || s2);

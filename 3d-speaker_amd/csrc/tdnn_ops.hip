@@ -9,6 +9,8 @@
 //  * cam_context      mean_T + 100-frame segment mean (ceil_mode)          campplus/layers.py:93-110
 //  * stats_pool       mean + unbiased std (no eps)                          campplus/layers.py:26-37
 #include "common.h"
+#include <cstdlib>
+
 #include "tdnn_ops.h"
 
 namespace spk {
@@ -253,6 +255,76 @@ cam_gate_kernel(const float* __restrict__ segsum, int T, int C, int seg, int nse
   }
 }
 
+// Lean form of cam_gate_kernel (CAMLayer context MLP, layers.py:40-67) for the shapes every
+// CAM++ layer has: 256 threads per utterance, the weights read straight from global memory
+// (row slices of 16 B quads, L2-resident: every utterance reads the same few KB) instead of
+// transposed into LDS per block, partial dots over Q = 256 / N contiguous K-slices combined by
+// a butterfly over the Q neighbouring lanes (fixed order).  Requires 256 % red == 0,
+// 256 % growth == 0, C % (4 * (256 / red)) == 0, red % (4 * (256 / growth)) == 0 (host).
+__global__ void __launch_bounds__(256)
+cam_gate_lean_kernel(const float* __restrict__ segsum, int T, int C, int seg, int nseg, const float* __restrict__ w1,
+                     int k1p, const float* __restrict__ b1, int red, const float* __restrict__ w2, int k2p,
+                     const float* __restrict__ b2, int growth, float* __restrict__ gate, int ldg,
+                     const int* __restrict__ vlen, const int* __restrict__ run_if) {
+  SPK_GATE(run_if);
+  extern __shared__ float sm[];
+  float* mean = sm;                         // [C]
+  float* ctx = mean + C;                    // [CAM_SEGS][C]
+  float* h = ctx + CAM_SEGS * C;            // [CAM_SEGS][red]
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int Tb = valid_frames(vlen, b, T);
+  const float* ss = segsum + (size_t)b * nseg * C;
+  for (int c = tid; c < C; c += 256) {
+    float v = 0.f;
+    for (int sg = 0; sg < nseg; ++sg) v += ss[(size_t)sg * C + c];
+    mean[c] = v / (float)Tb;
+  }
+  // out[j][n] = act(bias[n] + sum_k w[n][k] in[j][k]): thread = (n, slice q of K / Q)
+  auto dense = [&](const float* in, int K, const float* w, int kp, int N, const float* bias, bool relu, int ns,
+                   float* out, int ldout) {
+    const int Q = 256 / N, n = tid / Q, q = tid % Q, kk = K / Q;
+    float acc[CAM_SEGS];
+#pragma unroll
+    for (int j = 0; j < CAM_SEGS; ++j) acc[j] = 0.f;
+    const float* wr = w + (size_t)n * kp + q * kk;
+    for (int k = 0; k < kk; k += 4) {
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(wr + k);
+#pragma unroll
+      for (int j = 0; j < CAM_SEGS; ++j) {
+        if (j < ns) {
+          const f32x4 iv = *reinterpret_cast<const f32x4*>(in + j * K + q * kk + k);
+          acc[j] += wv[0] * iv[0] + wv[1] * iv[1] + wv[2] * iv[2] + wv[3] * iv[3];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CAM_SEGS; ++j)
+      for (int m = 1; m < Q; m <<= 1) acc[j] += __shfl_xor(acc[j], m);   // the Q lanes of n are adjacent
+    if (q == 0) {
+#pragma unroll
+      for (int j = 0; j < CAM_SEGS; ++j) {
+        if (j < ns) {
+          const float v = acc[j] + (bias ? bias[n] : 0.f);
+          out[(size_t)j * ldout + n] = relu ? fmaxf(v, 0.f) : __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+        }
+      }
+    }
+  };
+  for (int s0 = 0; s0 < nseg; s0 += CAM_SEGS) {
+    const int ns = min(CAM_SEGS, nseg - s0);
+    __syncthreads();                                       // mean ready / previous chunk's h read
+    for (int e = tid; e < ns * C; e += 256) {
+      const int j = e / C, c = e - j * C;
+      const int t0 = (s0 + j) * seg, t1 = min(Tb, t0 + seg);
+      ctx[e] = t1 > t0 ? mean[c] + ss[(size_t)(s0 + j) * C + c] / (float)(t1 - t0) : 0.f;
+    }
+    __syncthreads();
+    dense(ctx, C, w1, k1p, red, b1, true, ns, h, red);
+    __syncthreads();
+    dense(h, red, w2, k2p, growth, b2, false, ns, gate + ((size_t)b * nseg + s0) * ldg, ldg);
+  }
+}
+
 __global__ void stats_pool_kernel(const float* __restrict__ x, int B, int T, int C, int ld, float* __restrict__ out,
                                   const int* __restrict__ vlen, const int* __restrict__ run_if) {
   SPK_GATE(run_if);
@@ -325,6 +397,16 @@ hipError_t launch_cam_gate(const float* x, int B, int T, int C, int ld, int seg,
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(cam_segsum_kernel, dim3(nseg, B), dim3(256), 0, s, x, T, C, ld, seg, nseg, segsum, vlen, launch_gate());
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  static const bool lean_off = std::getenv("SPK_CAM_GATE_LDS") != nullptr;   // A/B: the transposing kernel
+  const bool lean = !lean_off && 256 % red == 0 && 256 % growth == 0 && C % (4 * (256 / red)) == 0 &&
+                    red % (4 * (256 / growth)) == 0 && k1p % 4 == 0 && k2p % 4 == 0 &&
+                    (reinterpret_cast<uintptr_t>(w1) & 15) == 0 && (reinterpret_cast<uintptr_t>(w2) & 15) == 0;
+  if (lean) {
+    const size_t lds_l = sizeof(float) * ((size_t)C + CAM_SEGS * ((size_t)C + red));
+    hipLaunchKernelGGL(cam_gate_lean_kernel, dim3(B), dim3(256), lds_l, s, segsum, T, C, seg, nseg, w1, k1p, b1, red,
+                       w2, k2p, b2, growth, gate, ldg, vlen, launch_gate());
+    return hipGetLastError();
+  }
   const size_t lds = sizeof(float) * ((size_t)C * (red + 1) + (size_t)red * (growth + 1) + C +
                                       CAM_SEGS * (C + red + 1024));
   if (lds > 64 * 1024) return hipErrorInvalidValue;
