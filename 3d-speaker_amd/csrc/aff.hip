@@ -43,10 +43,7 @@ __device__ __forceinline__ void split8(const f32x4 a, const f32x4 b, f16x8& hi, 
 __device__ __forceinline__ f16x8 ld_h8(const uint16_t* p) { return *reinterpret_cast<const f16x8*>(p); }
 __device__ __forceinline__ f16x4 ld_h4(const uint16_t* p) { return *reinterpret_cast<const f16x4*>(p); }
 
-constexpr int SLAB_LD = 36;
-#ifndef AFF_PF
-#define AFF_PF 3   // [x | y] k-steps in flight in stage 1
-#endif   // LDS row stride of the per-wave 32 x 32 transpose slab (floats)
+constexpr int SLAB_LD = 36;   // LDS row stride of the per-wave 32 x 32 transpose slab (floats)
 
 template <int MT>   // bottleneck tiles of 32 channels
 __global__ void __launch_bounds__(256) aff_x3_kernel(const AffDesc a) {
@@ -68,59 +65,45 @@ __global__ void __launch_bounds__(256) aff_x3_kernel(const AffDesc a) {
   for (int t = 0; t < MT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) { h[t][r] = 0.f; hx[t][r] = 0.f; }
-  // A ring of AFF_PF 32-deep k-steps in flight: each slot holds the step's [x | y] quads AND
-  // its W1 fragments, all requested together AFF_PF steps ahead (unconditional, clamped
-  // addresses; past K the B operand is zeroed), so the wait for a slot is a counted vmcnt
-  // that leaves the newer slots in flight.  (A W1 load issued at its use would retire every
-  // ring load in front of it: loads complete in order.)  Residency is capped at two blocks per
-  // CU, so the ring's registers are there.
-  struct Slot {
-    f32x4 v[2][2];
-    f16x8 wh[MT][2], wl[MT][2];
-  };
-  auto load_step = [&](int k0, Slot& sl) {
+  // [x | y] loads run one 32-deep step ahead of the MFMAs (clamped in-row addresses,
+  // zeroed past K when used, so the prefetch is unconditional)
+  auto load_xy = [&](int k0, f32x4 (&v)[2][2]) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {                   // 8 channels each, from x or y (cp % 8 == 0)
       const int k = min(k0 + 16 * lh + 8 * s, K - 8);
       const float* src = k < a.cp ? xr + k : yr + (k - a.cp);
-      sl.v[s][0] = *reinterpret_cast<const f32x4*>(src);
-      sl.v[s][1] = *reinterpret_cast<const f32x4*>(src + 4);
-#pragma unroll
-      for (int t = 0; t < MT; ++t) {                // k + 7 < K <= kp1: inside the packed row
-        const size_t wo = (size_t)(t * 32 + li) * a.kp1 + k;
-        sl.wh[t][s] = ld_h8(a.w1h + wo);
-        sl.wl[t][s] = ld_h8(a.w1l + wo);
-      }
+      v[s][0] = *reinterpret_cast<const f32x4*>(src);
+      v[s][1] = *reinterpret_cast<const f32x4*>(src + 4);
     }
   };
-  Slot ring[AFF_PF];
+  f32x4 vn[2][2];
+  load_xy(0, vn);
+  for (int k0 = 0; k0 < K; k0 += 32) {
+    f32x4 v[2][2];
 #pragma unroll
-  for (int p = 0; p < AFF_PF; ++p) load_step(32 * p, ring[p]);
-  for (int k0 = 0; k0 < K; k0 += 32 * AFF_PF) {
+    for (int s = 0; s < 2; ++s) {
+      const bool kin = k0 + 16 * lh + 8 * s < K;
+      v[s][0] = kin ? vn[s][0] : f32x4{0.f, 0.f, 0.f, 0.f};
+      v[s][1] = kin ? vn[s][1] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    load_xy(min(k0 + 32, K - 8), vn);
 #pragma unroll
-    for (int p = 0; p < AFF_PF; ++p) {
-      const int kk = k0 + 32 * p;
-      f16x8 bh[2], bl[2], ah[MT][2], al[MT][2];
+    for (int s = 0; s < 2; ++s) {
+      const int k = k0 + 16 * lh + 8 * s;
+      f16x8 bh, bl;
+      split8(v[s][0], v[s][1], bh, bl);
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bool kin = kk + 16 * lh + 8 * s < K;  // past K: zeros
-        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-        split8(kin ? ring[p].v[s][0] : z, kin ? ring[p].v[s][1] : z, bh[s], bl[s]);
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-          ah[t][s] = ring[p].wh[t][s];
-          al[t][s] = ring[p].wl[t][s];
+      for (int t = 0; t < MT; ++t) {
+        f16x8 ah = {}, al = {};
+        if (k < K) {                                // k + 7 < K <= kp1: inside the packed row
+          const size_t wo = (size_t)(t * 32 + li) * a.kp1 + k;
+          ah = ld_h8(a.w1h + wo);
+          al = ld_h8(a.w1l + wo);
         }
+        h[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, h[t], 0, 0, 0);
+        hx[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, hx[t], 0, 0, 0);
+        hx[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, hx[t], 0, 0, 0);
       }
-      load_step(kk + 32 * AFF_PF, ring[p]);       // clamped past K: re-reads the last step
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-          h[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t][s], bh[s], h[t], 0, 0, 0);
-          hx[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t][s], bl[s], hx[t], 0, 0, 0);
-          hx[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[t][s], bh[s], hx[t], 0, 0, 0);
-        }
     }
   }
 
@@ -132,7 +115,7 @@ __global__ void __launch_bounds__(256) aff_x3_kernel(const AffDesc a) {
     for (int r = 0; r < 16; ++r) {
       const int j = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
       float v = h[t][r] + hx[t][r] * (1.0f / 2048.0f) + a.b1[j];
-      v = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));         // SiLU
+      v = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));   // SiLU (hardware reciprocal)
       const _Float16 vh = (_Float16)v;
       gh[t][r >> 3][r & 7] = vh;
       gl[t][r >> 3][r & 7] = (_Float16)((v - (float)vh) * 2048.0f);

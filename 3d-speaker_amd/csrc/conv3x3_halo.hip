@@ -26,6 +26,9 @@
 #ifndef SPK_EXP
 #define SPK_EXP 0
 #endif
+#ifndef SPK_HALO_PF2
+#define SPK_HALO_PF2 0   // two halos in flight: measured neutral on ERes2NetV2, slower on ERes2Net-large / CAM++
+#endif
 
 namespace spk {
 
@@ -379,8 +382,13 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
     hrc[r] = (idx < hq && qq < C::Q) ? ((uint32_t)(p / HW) << 16) | (uint32_t)(p % HW) : 0x7FFF0000u;
   }
   const size_t img_px = (size_t)Hin * Win;
-  f32x4 pa[C::PF], pb[ADD ? C::PF : 1];
-  auto pf_load = [&](int t) {
+  // SPK_HALO_PF2: two tiles' halos in flight (register sets 0 / 1, the loop unrolled by two so
+  // the set is a compile-time index): a tile's halo is requested at the start of the tile two
+  // ahead, i.e. a whole tile earlier than with one set
+  constexpr int NSET = SPK_HALO_PF2 ? 2 : 1;
+  f32x4 pa[NSET][C::PF], pb[NSET][ADD ? C::PF : 1];
+  auto pf_load = [&](int t, auto setc) {
+    constexpr int S = decltype(setc)::value;
     const int img = t / (ntx * nty), ty = (t / ntx) % nty, tx = t % ntx;
     const int y0 = ty * TH * SH - 1, x0 = tx * TW - 1;
     const __amdgpu_buffer_rsrc_t r0 = make_rsrc(d.s0.p + img * img_px * d.s0.ld);
@@ -396,21 +404,22 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
       // some paths leaves its wait count unknown, and every later wait becomes vmcnt(0))
       uint32_t oa = ok ? (pix * (uint32_t)d.s0.ld + 4u * qq) * 4u : BUF_OOB;
       asm volatile("" : "+v"(oa));
-      pa[r] = buf_load4(r0, oa);
+      pa[S][r] = buf_load4(r0, oa);
       if (ADD) {
         uint32_t ob = ok ? (pix * (uint32_t)d.s0.ld2 + 4u * qq) * 4u : BUF_OOB;
         asm volatile("" : "+v"(ob));
-        pb[r] = buf_load4(r2, ob);
+        pb[S][r] = buf_load4(r2, ob);
       }
     }
   };
-  auto pf_store = [&]() {
+  auto pf_store = [&](auto setc) {
+    constexpr int S = decltype(setc)::value;
 #pragma unroll
     for (int r = 0; r < C::PF; ++r) {
       const int idx = tid + C::NT * r;
       if (idx < hq) {
-        f32x4 v = pa[r];
-        if (ADD) v += pb[r];
+        f32x4 v = pa[S][r];
+        if (ADD) v += pb[S][r];
         const int q = qq, p = idx / C::QP;
         f16x4 h, l;
         split_x3(v, h, l);
@@ -419,6 +428,8 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
       }
     }
   };
+  using Set0 = std::integral_constant<int, 0>;
+  using Set1 = std::integral_constant<int, NSET - 1>;
 
   // the epilogue's bias quad, loaded once, before the first halo prefetch so that
   // the first wait for the halo retires it too (otherwise the compiler keeps it pending and
@@ -430,7 +441,7 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
     if (d.bias && n < d.N) bias4 = *reinterpret_cast<const f32x4*>(d.bias + n);
   }
   int t = tbase;
-  if (t < ntiles) pf_load(t);
+  if (t < ntiles) pf_load(t, Set0{});
   // all nine taps of this slice's split weights -> LDS ([tap][n][ROW] hi / lo); zero padded
   for (int idx = tid; idx < 9 * C::NP * C::QP; idx += C::NT) {
     const int q = idx % C::QP, n = (idx / C::QP) % C::NP, tap = idx / (C::QP * C::NP);
@@ -444,17 +455,26 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
     *reinterpret_cast<u16x4*>(wh + (tap * C::NP + n) * C::ROW + 4 * q) = h;
     *reinterpret_cast<u16x4*>(wl + (tap * C::NP + n) * C::ROW + 4 * q) = l;
   }
-  if (t < ntiles) pf_store();
+  if (t < ntiles) pf_store(Set0{});
+  if (NSET == 2 && t + tstride < ntiles) pf_load(t + tstride, Set1{});
   __syncthreads();
 
   const int kg = wave / C::NW, pw = wave % C::NW;                  // k-group, pixel wave
   const int p_own = pw * 32 + li;
   const int abase = ((p_own / TW) * SH * HW + (p_own % TW)) * C::ROW + 8 * lh + 16 * C::KSG * kg;
   const int bbase = li * C::ROW + 8 * lh + 16 * C::KSG * kg;
-  for (; t < ntiles; t += tstride) {
+  // one tile; S = the register set this tile's successor-but-one is loaded into
+  auto tile = [&](int t, auto setc) {
+    constexpr int S = decltype(setc)::value;
     const int tn = t + tstride;
 #if SPK_EXP != 1
-    if (tn < ntiles) pf_load(tn);                   // in flight during the taps and epilogue
+    if (NSET == 2) {                                // in flight during this tile and the next
+      // unconditional (past the end: the last tile again), so the loads are on every path
+      // and the wait for the older set is a count that leaves these in flight
+      pf_load(min(tn + tstride, ntiles - 1), setc);
+    } else if (tn < ntiles) {                       // in flight during the taps and epilogue
+      pf_load(tn, setc);
+    }
 #endif
     f32x16 acc[1][1], accx;
 #pragma unroll
@@ -476,34 +496,93 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
     }
     acc[0][0] += accx * (1.0f / 2048.0f);
     __syncthreads();                                // halo reads done: the epilogue reuses it
-    if constexpr (KS > 1) {                         // group 1's partial sums -> group 0
-      float* part = lds + (C::NW + pw) * 1024;
-      if (kg == 1) {
+    const int img = t / (ntx * nty), ty = (t / ntx) % nty, tx = t % ntx;
+    const int y0 = ty * TH, x0 = tx * TW;
+    if constexpr (KS > 1 && PLAIN) {
+      // balanced epilogue: both k-groups' partial sums go to LDS (MFMA C layout, rows =
+      // pixels), then every wave finishes half the rows of its pixel tile (group kg: rows
+      // 16 kg .. 16 kg + 15) -- bias, activation, two row-quad stores per lane -- so all
+      // eight waves store (one group used to idle through the epilogue) and every wave issues
+      // the same stores, which keeps the next halos' wait counts exact
+      float* slab = lds + (kg * C::NW + pw) * 1024;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) part[r * 64 + lane] = acc[0][0][r];
-      }
+      for (int r = 0; r < 16; ++r) slab[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[0][0][r];
       __syncthreads();
-      if (kg == 0) {
+      const float* s0 = lds + pw * 1024;
+      const float* s1 = lds + (C::NW + pw) * 1024;
+      const int c4 = (lane & 7) * 4, n = n0 + c4, M = d.nimg * H * W;
+      float amax = 0.f;
+      f32x4 o[2];
+      int mq[2];
+      auto act_rows = [&](auto actc) {
+        constexpr int A = decltype(actc)::value;   // -1: general
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[0][0][r] += part[r * 64 + lane];
-      }
-    }
-    if (kg == 0) {
-      const int img = t / (ntx * nty), ty = (t / ntx) % nty, tx = t % ntx;
-      const int y0 = ty * TH, x0 = tx * TW;
+        for (int q = 0; q < 2; ++q) {
+          const int rl = 16 * kg + 8 * q + (lane >> 3);
+          const int p = pw * 32 + rl;
+          const int gy = y0 + p / TW, gx = x0 + p % TW;
+          mq[q] = (gy < H && gx < W) ? (img * H + gy) * W + gx : -1;
+          // group 0's partial + group 1's, then the bias: the order the two-step form used
+          o[q] = *reinterpret_cast<const f32x4*>(s0 + rl * 32 + c4) + *reinterpret_cast<const f32x4*>(s1 + rl * 32 + c4) +
+                 bias4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if constexpr (A >= 0) o[q][e] = apply_act(o[q][e], A);
+            else o[q][e] = apply_act(apply_act(o[q][e], d.act), d.act2);
+          }
+        }
+      };
+      if (d.act2 == ACT_NONE && d.act == ACT_HTANH) act_rows(std::integral_constant<int, ACT_HTANH>{});
+      else if (d.act2 == ACT_NONE && d.act == ACT_RELU) act_rows(std::integral_constant<int, ACT_RELU>{});
+      else act_rows(std::integral_constant<int, -1>{});
 #if SPK_EXP != 2
-      epilogue_tiles<1, 1, true, PLAIN>(d, lds, acc, pw, lane, n0, d.nimg * H * W, [&](int r) {
-        const int p = pw * 32 + r;
-        const int gy = y0 + p / TW, gx = x0 + p % TW;
-        return (gy < H && gx < W) ? (img * H + gy) * W + gx : -1;
-      }, &bias4);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (n < d.N && mq[q] >= 0 && mq[q] < M) {
+          amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[q][0]), fabsf(o[q][1])), fmaxf(fabsf(o[q][2]), fabsf(o[q][3]))));
+          *reinterpret_cast<f32x4*>(d.out + (size_t)mq[q] * d.ldo + n) = o[q];
+        }
+      }
+      range_note(d.range_flag, amax);
 #else
-      if (acc[0][0][0] == 12345.f) d.out[img + y0 + x0] = 1.f;
+      if (o[0][0] == 12345.f) d.out[img + y0 + x0] = 1.f;
 #endif
+    } else {
+      if constexpr (KS > 1) {                       // group 1's partial sums -> group 0
+        float* part = lds + (C::NW + pw) * 1024;
+        if (kg == 1) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) part[r * 64 + lane] = acc[0][0][r];
+        }
+        __syncthreads();
+        if (kg == 0) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[0][0][r] += part[r * 64 + lane];
+        }
+      }
+      if (kg == 0) {
+#if SPK_EXP != 2
+        epilogue_tiles<1, 1, true, PLAIN>(d, lds, acc, pw, lane, n0, d.nimg * H * W, [&](int r) {
+          const int p = pw * 32 + r;
+          const int gy = y0 + p / TW, gx = x0 + p % TW;
+          return (gy < H && gx < W) ? (img * H + gy) * W + gx : -1;
+        }, &bias4);
+#else
+        if (acc[0][0][0] == 12345.f) d.out[img + y0 + x0] = 1.f;
+#endif
+      }
     }
     __syncthreads();                                // epilogue LDS reads done
-    if (tn < ntiles) pf_store();
+    if (tn < ntiles) pf_store(std::integral_constant<int, NSET == 2 ? 1 - S : 0>{});
     __syncthreads();
+  };
+  if constexpr (NSET == 2) {
+    for (; t < ntiles; t += 2 * tstride) {
+      tile(t, Set0{});
+      if (t + tstride < ntiles) tile(t + tstride, Set1{});
+    }
+  } else {
+    for (; t < ntiles; t += tstride) tile(t, Set0{});
   }
 }
 
