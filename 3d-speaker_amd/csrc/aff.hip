@@ -121,23 +121,28 @@ __global__ void __launch_bounds__(256) aff_x3_kernel(const AffDesc a) {
       gl[t][r >> 3][r & 7] = (_Float16)((v - (float)vh) * 2048.0f);
     }
 
-  // ---- stage 2 + AFF combine, 32 output channels at a time
-  for (int n0 = 0; n0 < a.cp; n0 += 32) {
-    const int n = min(n0 + li, a.cp - 1);           // W2 row of this lane (A operand)
-    const bool nok = n0 + li < a.cp;
-    // the combine works on whole 128-B row segments (8 lanes per pixel row, 4 rows per
-    // pass): x / y of those are requested before the MFMAs
-    const int c4 = (lane & 7) * 4, cc = min(n0 + c4, a.cp - 4);
+  // ---- stage 2 + AFF combine, 32 output channels at a time.  A chunk's operands -- the
+  // x / y row segments of the combine and the W2 fragments -- are requested one chunk ahead
+  // (clamped, unconditional: the last chunk re-reads itself), so each chunk's waits are
+  // counts that leave the next chunk's loads in flight
+  const int c4 = (lane & 7) * 4;
+  const int nch = (a.cp + 31) / 32;                 // <= 7 (cp <= 208)
+  struct Chunk {
     f32x4 xv[4], yv[4];
+    f16x8 wh[MT][2], wl[MT][2];
+    f32x4 b2;
+  };
+  auto load_chunk = [&](int c, Chunk& ck) {
+    const int n0 = 32 * c;
+    const int n = min(n0 + li, a.cp - 1);           // W2 row of this lane (A operand)
+    const int cc = min(n0 + c4, a.cp - 4);
+    ck.b2 = *reinterpret_cast<const f32x4*>(a.b2 + cc);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int mq = min(m0 + q * 8 + (lane >> 3), a.M - 1);
-      xv[q] = *reinterpret_cast<const f32x4*>(a.x + (size_t)mq * a.ldx + cc);
-      yv[q] = *reinterpret_cast<const f32x4*>(a.y + (size_t)mq * a.ldy + cc);
+      ck.xv[q] = *reinterpret_cast<const f32x4*>(a.x + (size_t)mq * a.ldx + cc);
+      ck.yv[q] = *reinterpret_cast<const f32x4*>(a.y + (size_t)mq * a.ldy + cc);
     }
-    f32x16 z, zx;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { z[r] = 0.f; zx[r] = 0.f; }
 #pragma unroll
     for (int t = 0; t < MT; ++t)
 #pragma unroll
@@ -145,9 +150,21 @@ __global__ void __launch_bounds__(256) aff_x3_kernel(const AffDesc a) {
         const size_t wo = (size_t)n * a.kp2 + t * 32 + 16 * s + 4 * lh;
         const f16x4 h0 = ld_h4(a.w2h + wo), h1 = ld_h4(a.w2h + wo + 8);
         const f16x4 l0 = ld_h4(a.w2l + wo), l1 = ld_h4(a.w2l + wo + 8);
-        f16x8 ah = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-        f16x8 al = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
-        if (!nok) { ah = f16x8{}; al = f16x8{}; }
+        ck.wh[t][s] = f16x8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        ck.wl[t][s] = f16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+      }
+  };
+  auto chunk = [&](int c, const Chunk& ck) {
+    const int n0 = 32 * c;
+    const bool nok = n0 + li < a.cp;
+    f32x16 z, zx;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { z[r] = 0.f; zx[r] = 0.f; }
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const f16x8 ah = nok ? ck.wh[t][s] : f16x8{}, al = nok ? ck.wl[t][s] : f16x8{};
         z = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gh[t][s], z, 0, 0, 0);
         zx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gl[t][s], zx, 0, 0, 0);
         zx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, gh[t][s], zx, 0, 0, 0);
@@ -159,7 +176,7 @@ __global__ void __launch_bounds__(256) aff_x3_kernel(const AffDesc a) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const f32x4 bias = *reinterpret_cast<const f32x4*>(a.b2 + cc);
+    const f32x4 bias = ck.b2;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int p = q * 8 + (lane >> 3);
@@ -169,7 +186,7 @@ __global__ void __launch_bounds__(256) aff_x3_kernel(const AffDesc a) {
       for (int e = 0; e < 4; ++e) {
         // x(1 + tanh z) + y(1 - tanh z) = 2(y + s(x - y)), s = sigmoid(2z): one exp + rcp
         const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * (zq[e] + bias[e])));
-        o[e] = 2.0f * fmaf(sg, xv[q][e] - yv[q][e], yv[q][e]);
+        o[e] = 2.0f * fmaf(sg, ck.xv[q][e] - ck.yv[q][e], ck.yv[q][e]);
       }
       if (m0 + p < a.M && n0 + c4 < a.cp) {
         amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
@@ -179,6 +196,23 @@ __global__ void __launch_bounds__(256) aff_x3_kernel(const AffDesc a) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // slab reads done before the next chunk
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  if constexpr (MT == 1) {
+    Chunk ring[2];
+    load_chunk(0, ring[0]);
+#pragma unroll
+    for (int c = 0; c < 7; ++c) {                   // unrolled: the set index is a constant
+      if (c >= nch) break;
+      load_chunk(min(c + 1, nch - 1), ring[(c + 1) & 1]);
+      chunk(c, ring[c & 1]);
+    }
+  } else {                                          // two bottleneck tiles: no room for a
+    Chunk ck;                                       // second set at two waves per SIMD
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c) {
+      load_chunk(c, ck);
+      chunk(c, ck);
+    }
   }
   range_note(a.range_flag, amax);
 }
