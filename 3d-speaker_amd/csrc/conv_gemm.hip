@@ -455,6 +455,10 @@ struct Cfg {
   int bm, bn, bk, wm, wn;
 };
 
+#ifndef SPK_DEEP_K
+#define SPK_DEEP_K 4096   // K from which the 256x128 tile is used
+#endif
+
 Cfg select_cfg(const ConvDesc& d) {
   const int M = d.nimg * d.Ho * d.Wo;
   const int bk = d.Kp >= 256 ? 32 : 16;
@@ -470,7 +474,7 @@ Cfg select_cfg(const ConvDesc& d) {
     // keeps two blocks (four waves per SIMD) per CU and is the fastest or within 2 % on every
     // x3 GEMM of ERes2NetV2 / ERes2Net-large (all-128x128 27.0 ms vs 28.6 for round 2's
     // per-layer mix); only the deepest K (the 4608-deep stage-3 downsample) keeps 256x128 (-5 %)
-    if (d.Kp >= 4096 && d.N >= 512) return {256, 128, 32, 4, 2};
+    if (d.Kp >= SPK_DEEP_K && d.N >= 512) return {256, 128, 32, 4, 2};
   }
   // 128x128 at BK=32 still fits two blocks per CU (73.7 KB LDS): half the K-steps, twice
   // the loads in flight per step -- what the short-K 1x1 convs need

@@ -27,7 +27,9 @@ ConvSrc src1d(int ld, int T, int cin, int k = 1, int dil = 1, bool reflect = fal
   s.ld = ld; s.H = 1; s.W = T; s.cin = cin;
   s.kh = 1; s.kw = k; s.dw = dil;
   s.pw = reflect ? dil * (k - 1) / 2 : 0;
-  s.reflect = reflect ? 1 : 0;
+  // a one-tap conv has no padding to reflect: flagging it would keep the 3072-deep MFA GEMM
+  // off the buffer-resource loader (conv_buf_loader_ok) for nothing
+  s.reflect = reflect && k > 1 ? 1 : 0;
   return s;
 }
 
