@@ -132,7 +132,9 @@ __host__ __device__ inline bool row_masked(const ConvDesc& d, int m) {
 // byte a block of `bm` rows can touch within 2 GiB of its first image.  Otherwise the
 // generic loader runs, which exists for the plain and the addend (ADD) forms only.
 inline bool conv_buf_loader_ok(const ConvDesc& d, int bm) {
-  if (d.s0.reflect || d.s0.cin < 32 || d.s0.kh * d.s0.kw > 30) return false;
+  // reflect padding: the 1-D form only (ECAPA's Conv1d, H = 1), full-length rows, pad < W
+  if (d.s0.reflect && !(d.s0.H == 1 && d.s0.kh == 1 && !d.s0.vlen && d.s0.pw < d.s0.W)) return false;
+  if (d.s0.cin < 32 || d.s0.kh * d.s0.kw > 30) return false;
   const double span = (double)(bm / (d.Ho * d.Wo) + 2);
   const double lim = 0x7FFFFFF0 - 64;
   if (span * d.s0.H * d.s0.W * d.s0.ld * 4.0 > lim) return false;

@@ -170,6 +170,7 @@ struct BufALoader {
   __amdgpu_buffer_rsrc_t r0, r2, r1;
   uint32_t roff[AROWS], roff2[ADD ? AROWS : 1], roff1[S1 ? AROWS : 1];
   uint32_t rmask[AROWS];   // bit t: tap t in bounds; bit 31: row < M
+  int wbr[AROWS];          // reflect padding (1-D, H = 1): the row's first tap column
   int c, t, kx, tdp;       // this thread's quad: channel within tap, tap, tap column, tap pixel delta
 
   __device__ __forceinline__ void init(const ConvDesc& d, int m0, int row0, int kq, int kt0) {
@@ -205,6 +206,10 @@ struct BufALoader {
           if (wi >= 0 && wi < wl) mk |= 1u << (ky * d.s0.kw + x);
         }
       }
+      // reflect padding (conv_buf_loader_ok: H = 1, kh = 1, no ragged rows): every tap reads
+      // a pixel of the row's image, the out-of-range ones mirrored at load time
+      if (d.s0.reflect) mk = (1u << d.s0.kw) - 1u;
+      wbr[r] = wb;
       rmask[r] = valid ? (mk | 0x80000000u) : 0u;
     }
     const int taps = d.s0.kh * d.s0.kw;
@@ -241,8 +246,16 @@ struct BufALoader {
 #pragma unroll
     for (int r = 0; r < AROWS; ++r) {
       const bool b = (rmask[r] >> t) & 1u;   // t <= taps <= 30: never the row bit
-      s.v[r] = buf_load4(r0, b ? roff[r] + toff : BUF_OOB);
-      if (ADD) s.v2[r] = buf_load4(r2, b ? roff2[r] + toff2 : BUF_OOB);
+      uint32_t o0 = roff[r] + toff, o2 = ADD ? roff2[r] + toff2 : 0u;
+      if (d.s0.reflect) {                    // mirrored column (selects, no branch around a load)
+        int wi = wbr[r] + kx * d.s0.dw;
+        wi = wi < 0 ? -wi : (wi >= d.s0.W ? 2 * d.s0.W - 2 - wi : wi);
+        const int dpx = wi - wbr[r];
+        o0 = roff[r] + (uint32_t)(dpx * d.s0.ld + c) * 4u;
+        if (ADD) o2 = roff2[r] + (uint32_t)(dpx * d.s0.ld2 + c) * 4u;
+      }
+      s.v[r] = buf_load4(r0, b ? o0 : BUF_OOB);
+      if (ADD) s.v2[r] = buf_load4(r2, b ? o2 : BUF_OOB);
       if (S1) s.v2[r] = buf_load4(r1, (in1 && (rmask[r] >> 31)) ? roff1[r] + (uint32_t)c * 4u : BUF_OOB);
       if (PRE) ok |= (unsigned)b << r;
     }
