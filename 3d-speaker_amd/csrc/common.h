@@ -96,6 +96,40 @@ constexpr float kX3WeightLimit = 31.5f;
 __device__ __forceinline__ void range_note(int* flag, float amax) {
   if (flag && amax >= kRangeLimit) atomicOr(flag, 1);
 }
+// Time reductions with one lane per channel (TDNN statistics, TSTP pooling) are latency-
+// bound: a frame's load feeds a serial update, so a wave keeps only a load or two in flight.
+// scan_frames issues U frames' loads back to back, then runs the updates in frame order
+// (results bit-identical to the frame-at-a-time loop).
+template <int U, class F>
+__device__ __forceinline__ void scan_frames(const float* p, size_t ld, int Tb, F f) {
+  int t = 0;
+  for (; t + U <= Tb; t += U) {
+    float v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = p[(size_t)(t + j) * ld];
+#pragma unroll
+    for (int j = 0; j < U; ++j) f(v[j], t + j);
+  }
+  for (; t < Tb; ++t) f(p[(size_t)t * ld], t);
+}
+
+// the same over two arrays read in step (logits and x of the attentive pooling)
+template <int U, class F>
+__device__ __forceinline__ void scan_frames2(const float* p, size_t ldp, const float* q, size_t ldq, int Tb, F f) {
+  int t = 0;
+  for (; t + U <= Tb; t += U) {
+    float a[U], b[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      a[j] = p[(size_t)(t + j) * ldp];
+      b[j] = q[(size_t)(t + j) * ldq];
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) f(a[j], b[j]);
+  }
+  for (; t < Tb; ++t) f(p[(size_t)t * ldp], q[(size_t)t * ldq]);
+}
+
 // launch gate: a kernel of the gated exact plan returns at once unless *run_if != 0 (the
 // word is not written while that plan runs, so every wave of the grid sees the same value)
 #define SPK_GATE(run_if) do { if ((run_if) != nullptr && *(run_if) == 0) return; } while (0)

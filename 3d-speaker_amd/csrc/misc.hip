@@ -99,12 +99,11 @@ tstp_kernel(const float* __restrict__ x, int B, int H, int W, int C, int ld, flo
     const float* p = x + ((size_t)(b * H + h) * W) * ld + c;
     // one Welford pass (mean, M2): the activation is read once, not twice
     float mean = 0.f, q = 0.f;
-    for (int t = 0; t < W; ++t) {
-      const float v = p[(size_t)t * ld];
+    scan_frames<16>(p, ld, W, [&](float v, int t) {
       const float dlt = v - mean;
       mean += dlt / (float)(t + 1);
       q = fmaf(dlt, v - mean, q);
-    }
+    });
     const float var = q / (float)(unbiased ? W - 1 : W);
     // parts: bit 0 = mean (TAP), bit 1 = std (TSDP); TSTP = both, mean first
     const int np = (parts & 1) + ((parts >> 1) & 1);

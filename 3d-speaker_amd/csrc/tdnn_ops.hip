@@ -38,7 +38,7 @@ __global__ void time_mean_kernel(const float* __restrict__ x, int B, int T, int 
     const int Tb = valid_frames(vlen, b, T);
     const float* p = x + (size_t)b * T * ld + c;
     float s = 0.f;
-    for (int t = 0; t < Tb; ++t) s += p[(size_t)t * ld];
+    scan_frames<16>(p, ld, Tb, [&](float v, int) { s += v; });
     out[(size_t)b * ldo + c] = s / (float)Tb;
   }
 }
@@ -53,12 +53,11 @@ __global__ void asp_stats_kernel(const float* __restrict__ x, int B, int T, int 
     const float* p = x + (size_t)b * T * ld + c;
     // one Welford pass (mean, M2) instead of two passes over x; var = M2 / T
     float mean = 0.f, m2 = 0.f;
-    for (int t = 0; t < Tb; ++t) {
-      const float xv = p[(size_t)t * ld];
+    scan_frames<16>(p, ld, Tb, [&](float xv, int t) {
       const float d = xv - mean;
       mean += d / (float)(t + 1);
       m2 += d * (xv - mean);
-    }
+    });
     out[(size_t)b * 2 * C + c] = mean;
     out[(size_t)b * 2 * C + C + c] = sqrtf(fmaxf(m2 / (float)Tb, eps));
   }
@@ -77,8 +76,7 @@ __global__ void attn_pool_kernel(const float* __restrict__ logit, int ldl, const
     // weighted Welford update of mean and M2 = sum w (x - mean)^2, so logits and x are read
     // once instead of four and two times; var = M2 / sum w (ECAPA_TDNN.py:276-287)
     float mx = -INFINITY, sw = 0.f, mean = 0.f, m2 = 0.f;
-    for (int t = 0; t < Tb; ++t) {
-      const float lv = l[(size_t)t * ldl], xv = p[(size_t)t * ldx];
+    scan_frames2<8>(l, ldl, p, ldx, Tb, [&](float lv, float xv) {
       if (lv > mx) {
         const float sc = __expf(mx - lv);           // 0 on the first sample
         sw *= sc;
@@ -90,7 +88,7 @@ __global__ void attn_pool_kernel(const float* __restrict__ logit, int ldl, const
       const float d = xv - mean;
       mean += d * (w / sw);
       m2 += w * d * (xv - mean);
-    }
+    });
     out[(size_t)b * 2 * C + c] = mean;
     out[(size_t)b * 2 * C + C + c] = sqrtf(fmaxf(m2 / sw, eps));
   }
@@ -334,12 +332,11 @@ __global__ void stats_pool_kernel(const float* __restrict__ x, int B, int T, int
     const int Tb = valid_frames(vlen, b, T);
     const float* p = x + (size_t)b * T * ld + c;
     float mean = 0.f, q = 0.f;                       // one Welford pass (mean, M2)
-    for (int t = 0; t < Tb; ++t) {
-      const float v = p[(size_t)t * ld];
+    scan_frames<16>(p, ld, Tb, [&](float v, int t) {
       const float d = v - mean;
       mean += d / (float)(t + 1);
       q += d * (v - mean);
-    }
+    });
     out[(size_t)b * 2 * C + c] = mean;
     out[(size_t)b * 2 * C + C + c] = sqrtf(q / (float)(Tb - 1));
   }
