@@ -19,6 +19,7 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int CAM_SEGS = 4;   // segments whose 1x1 layers run together (weights read once)
+constexpr int CAM_WQ = 8;     // lean gate: float4 quads of a thread's weight slice per layer
 
 inline int grid_for(long long n) { return (int)std::min<long long>((n + 255) / 256, 65536); }
 
@@ -272,25 +273,41 @@ cam_gate_lean_kernel(const float* __restrict__ segsum, int T, int C, int seg, in
   const int b = blockIdx.x, tid = threadIdx.x;
   const int Tb = valid_frames(vlen, b, T);
   const float* ss = segsum + (size_t)b * nseg * C;
+  // this thread's weight slices and biases of both layers, requested first: the phases below
+  // are a chain of dependent steps, and a weight load at its use was one more L2 round trip
+  // in it (host: K / Q <= 4 * CAM_WQ for both layers)
+  f32x4 wq1[CAM_WQ], wq2[CAM_WQ];
+  float bq1 = 0.f, bq2 = 0.f;
+  auto load_w = [&](const float* w, int kp, int K, int N, const float* bias, f32x4 (&wq)[CAM_WQ], float& bq) {
+    const int Q = 256 / N, n = tid / Q, q = tid % Q, kk = K / Q;
+    const float* wr = w + (size_t)n * kp + q * kk;
+#pragma unroll
+    for (int i = 0; i < CAM_WQ; ++i)
+      wq[i] = 4 * i < kk ? *reinterpret_cast<const f32x4*>(wr + 4 * i) : f32x4{0.f, 0.f, 0.f, 0.f};
+    bq = bias ? bias[n] : 0.f;
+  };
+  load_w(w1, k1p, C, red, b1, wq1, bq1);
+  load_w(w2, k2p, red, growth, b2, wq2, bq2);
   for (int c = tid; c < C; c += 256) {
     float v = 0.f;
     for (int sg = 0; sg < nseg; ++sg) v += ss[(size_t)sg * C + c];
     mean[c] = v / (float)Tb;
   }
   // out[j][n] = act(bias[n] + sum_k w[n][k] in[j][k]): thread = (n, slice q of K / Q)
-  auto dense = [&](const float* in, int K, const float* w, int kp, int N, const float* bias, bool relu, int ns,
+  auto dense = [&](const float* in, int K, const f32x4 (&wq)[CAM_WQ], float bq, int N, bool relu, int ns,
                    float* out, int ldout) {
     const int Q = 256 / N, n = tid / Q, q = tid % Q, kk = K / Q;
     float acc[CAM_SEGS];
 #pragma unroll
     for (int j = 0; j < CAM_SEGS; ++j) acc[j] = 0.f;
-    const float* wr = w + (size_t)n * kp + q * kk;
-    for (int k = 0; k < kk; k += 4) {
-      const f32x4 wv = *reinterpret_cast<const f32x4*>(wr + k);
+#pragma unroll
+    for (int i = 0; i < CAM_WQ; ++i) {
+      if (4 * i >= kk) break;
+      const f32x4 wv = wq[i];
 #pragma unroll
       for (int j = 0; j < CAM_SEGS; ++j) {
         if (j < ns) {
-          const f32x4 iv = *reinterpret_cast<const f32x4*>(in + j * K + q * kk + k);
+          const f32x4 iv = *reinterpret_cast<const f32x4*>(in + j * K + q * kk + 4 * i);
           acc[j] += wv[0] * iv[0] + wv[1] * iv[1] + wv[2] * iv[2] + wv[3] * iv[3];
         }
       }
@@ -302,7 +319,7 @@ cam_gate_lean_kernel(const float* __restrict__ segsum, int T, int C, int seg, in
 #pragma unroll
       for (int j = 0; j < CAM_SEGS; ++j) {
         if (j < ns) {
-          const float v = acc[j] + (bias ? bias[n] : 0.f);
+          const float v = acc[j] + bq;
           out[(size_t)j * ldout + n] = relu ? fmaxf(v, 0.f) : __builtin_amdgcn_rcpf(1.0f + __expf(-v));
         }
       }
@@ -317,9 +334,9 @@ cam_gate_lean_kernel(const float* __restrict__ segsum, int T, int C, int seg, in
       ctx[e] = t1 > t0 ? mean[c] + ss[(size_t)(s0 + j) * C + c] / (float)(t1 - t0) : 0.f;
     }
     __syncthreads();
-    dense(ctx, C, w1, k1p, red, b1, true, ns, h, red);
+    dense(ctx, C, wq1, bq1, red, true, ns, h, red);
     __syncthreads();
-    dense(h, red, w2, k2p, growth, b2, false, ns, gate + ((size_t)b * nseg + s0) * ldg, ldg);
+    dense(h, red, wq2, bq2, growth, false, ns, gate + ((size_t)b * nseg + s0) * ldg, ldg);
   }
 }
 
@@ -396,7 +413,8 @@ hipError_t launch_cam_gate(const float* x, int B, int T, int C, int ld, int seg,
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   static const bool lean_off = std::getenv("SPK_CAM_GATE_LDS") != nullptr;   // A/B: the transposing kernel
   const bool lean = !lean_off && 256 % red == 0 && 256 % growth == 0 && C % (4 * (256 / red)) == 0 &&
-                    red % (4 * (256 / growth)) == 0 && k1p % 4 == 0 && k2p % 4 == 0 &&
+                    red % (4 * (256 / growth)) == 0 && C / (256 / red) <= 4 * CAM_WQ &&
+                    red / (256 / growth) <= 4 * CAM_WQ && k1p % 4 == 0 && k2p % 4 == 0 &&
                     (reinterpret_cast<uintptr_t>(w1) & 15) == 0 && (reinterpret_cast<uintptr_t>(w2) & 15) == 0;
   if (lean) {
     const size_t lds_l = sizeof(float) * ((size_t)C + CAM_SEGS * ((size_t)C + red));
