@@ -19,7 +19,13 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int CAM_SEGS = 4;   // segments whose 1x1 layers run together (weights read once)
-constexpr int CAM_WQ = 8;     // lean gate: float4 quads of a thread's weight slice per layer
+constexpr int CAM_WQ = 8;
+#ifndef SPK_SEGSUM_U
+#define SPK_SEGSUM_U 4   // cam_segsum: row loads in flight per thread
+#endif
+#ifndef SPK_ATTN_U
+#define SPK_ATTN_U 8     // attn_pool: frames per load batch
+#endif     // lean gate: float4 quads of a thread's weight slice per layer
 
 inline int grid_for(long long n) { return (int)std::min<long long>((n + 255) / 256, 65536); }
 
@@ -77,7 +83,7 @@ __global__ void attn_pool_kernel(const float* __restrict__ logit, int ldl, const
     // weighted Welford update of mean and M2 = sum w (x - mean)^2, so logits and x are read
     // once instead of four and two times; var = M2 / sum w (ECAPA_TDNN.py:276-287)
     float mx = -INFINITY, sw = 0.f, mean = 0.f, m2 = 0.f;
-    scan_frames2<8>(l, ldl, p, ldx, Tb, [&](float lv, float xv) {
+    scan_frames2<SPK_ATTN_U>(l, ldl, p, ldx, Tb, [&](float lv, float xv) {
       if (lv > mx) {
         const float sc = __expf(mx - lv);           // 0 on the first sample
         sw *= sc;
@@ -162,12 +168,12 @@ cam_segsum_kernel(const float* __restrict__ x, int T, int C, int ld, int seg, in
   if (rl < RL) {
     const float* xb = x + (size_t)b * T * ld + cq * 4;
     int t = t0 + rl;
-    for (; t + 3 * RL < t1; t += 4 * RL) {
-      const f32x4 q0 = *reinterpret_cast<const f32x4*>(xb + (size_t)t * ld);
-      const f32x4 q1 = *reinterpret_cast<const f32x4*>(xb + (size_t)(t + RL) * ld);
-      const f32x4 q2 = *reinterpret_cast<const f32x4*>(xb + (size_t)(t + 2 * RL) * ld);
-      const f32x4 q3 = *reinterpret_cast<const f32x4*>(xb + (size_t)(t + 3 * RL) * ld);
-      a += q0; a += q1; a += q2; a += q3;
+    for (; t + (SPK_SEGSUM_U - 1) * RL < t1; t += SPK_SEGSUM_U * RL) {
+      f32x4 q[SPK_SEGSUM_U];
+#pragma unroll
+      for (int j = 0; j < SPK_SEGSUM_U; ++j) q[j] = *reinterpret_cast<const f32x4*>(xb + (size_t)(t + j * RL) * ld);
+#pragma unroll
+      for (int j = 0; j < SPK_SEGSUM_U; ++j) a += q[j];
     }
     for (; t < t1; t += RL) a += *reinterpret_cast<const f32x4*>(xb + (size_t)t * ld);
   }
