@@ -76,6 +76,9 @@ struct ConvDesc {
   // block, and the taps of a block follow each other, so the block's input pixels are re-read
   // from L2 within a few K-tiles instead of once per sweep over the whole K (runtime.cpp pack)
   int kcb = 0;
+  // the weights in MFMA fragment order for the LDS-DMA GEMM (conv_gemm_f.hip launch_pack_frag;
+  // null: that kernel is not used)
+  const uint16_t* wf = nullptr;
 };
 
 // fp16x3 range guard.  The split-precision GEMMs represent an operand as two fp16 values,
@@ -190,6 +193,14 @@ hipError_t launch_splitk_reduce(const ConvDesc& d, hipStream_t s);   // conv_gem
 bool pw_supported(const ConvDesc& d);
 hipError_t launch_pw(const ConvDesc& d, hipStream_t s);
 std::string pw_kernel_name(const ConvDesc& d);   // blocks of one split of the tile config launch_conv picks
+
+// fp16x3 GEMM with fragment-packed weights streamed by LDS-DMA (conv_gemm_f.hip); launch_conv
+// routes the plain buffer-loader layers to it
+bool gemm_f_supported(const ConvDesc& d);
+hipError_t launch_gemm_f(const ConvDesc& d, hipStream_t s);
+std::string gemm_f_kernel_name(const ConvDesc& d);
+size_t frag_halves(int N, int Kp);   // size of one matrix in fragment order (N padded to 128)
+hipError_t launch_pack_frag(const uint16_t* wh, const uint16_t* wl, int N, int Kp, uint16_t* out, hipStream_t s);
 
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 

@@ -362,6 +362,7 @@ __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
       // even step: LDS buffer 0 holds kt, set 1 holds kt+1 (in flight), set 0 is free
 #if SPK_GEXP != 3
       load_tile(min(kt + 2, kt1 - 1), set0);
+#endif
       compute(0);
 #if SPK_GEXP != 5
       if (UNCOND || kt + 1 < kt1) store_tile(1, set1);
@@ -379,7 +380,6 @@ __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
       __syncthreads();
     }
   }
-#endif
   if constexpr (!X1) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -532,6 +532,7 @@ hipError_t launch_bk(const ConvDesc& d, const Cfg& c, hipStream_t s) {
 std::string conv_kernel_name(const ConvDesc& d) {
   if (halo_conv_supported(d)) return halo_kernel_name(d);
   if (use_x3() && pw_supported(d)) return pw_kernel_name(d);
+  if (use_x3() && gemm_f_supported(d)) return gemm_f_kernel_name(d);
   const Cfg c = select_cfg(d);
   const bool s1 = d.s1.p != nullptr || d.s1.cin > 0, add = d.s0.p2 != nullptr || d.s0.ld2 > 0;
   const bool pre = d.s0.pre_scale != nullptr;
@@ -565,6 +566,7 @@ hipError_t launch_conv(const ConvDesc& dd, hipStream_t s) {
     return hipErrorInvalidValue;
   if (halo_conv_supported(d)) return launch_conv3x3_halo(d, s);
   if (use_x3() && pw_supported(d)) return launch_pw(d, s);
+  if (use_x3() && gemm_f_supported(d)) return launch_gemm_f(d, s);
   const Cfg c = select_cfg(d);
   return c.bk == 32 ? launch_bk<32>(d, c, s) : launch_bk<16>(d, c, s);
 }

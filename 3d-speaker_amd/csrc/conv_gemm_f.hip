@@ -1,0 +1,353 @@
+// fp16x3 implicit-GEMM convolution with fragment-packed weights streamed into LDS by
+// LDS-DMA (gfx950).  The common layers of the ERes2Net(V2) stages 3-4 and every other plain
+// conv the buffer-resource loader serves (conv_loader.h BufALoader conditions, no
+// K-concatenated second operand, no BN-ReLU pre-activation).
+//
+// What differs from the register-staged kernel (conv_gemm.hip conv_gemm_x3_kernel):
+//   * B (weights) never passes through VGPRs.  At model creation every packed weight matrix
+//     is also laid out in MFMA fragment order (launch_pack_frag): per 32-deep K-tile, per
+//     32-column n-tile, per 16-deep k-step, per plane (fp16 hi, fp16 lo) one 1-KB chunk whose
+//     16-B lane slots are exactly the B operand of v_mfma_f32_32x32x16_f16.  A block's 16
+//     chunks of a K-tile are contiguous; each wave moves two of them with
+//     `buffer_load_dwordx4 ... lds` (no VGPR destination, no ds_write, no waits of its own)
+//     and reads its fragments back with conflict-free ds_read_b128 (lane-linear 1-KB rows).
+//   * A (fp32 activations) is staged through registers as before -- the fp16 hi / lo split
+//     happens once per element, in the staging pass -- but the K walk is scalar: the K-tile
+//     start (tap t0, channel c0) and the pixel deltas of taps t0 and t0 + 1 are wave-uniform
+//     (SGPRs); a lane's quad is past the tap boundary or not (one compare, two selects), so
+//     the loop body has no lane-divergent branch and no runtime-optional path (reflect padding,
+//     channel-block K order, K-concatenated operands stay on the older kernel).
+//   * The DMA is issued by inline asm, invisible to hipcc's wait counting: issued before the
+//     K-tile's A loads, the compiler's counted wait for the previous A set also retires it
+//     (vmcnt retires in order), and an explicit `s_waitcnt vmcnt(<A loads>)` before the
+//     barrier makes that independent of the schedule.  (A DMA the compiler can see makes it
+//     drain vmcnt(0) at every use of an ordinary load: cdna_hip_programming.md §5.)
+// Numerics are those of the register-staged fp16x3 kernel (same split, same one-accumulator
+// products, same K order): x w ~= 2^-11 (hi_x (2^11 hi_w) + hi_x lo_w + lo_x hi_w).
+#include <cstdlib>
+#include <string>
+
+#include "common.h"
+#include "conv_epilogue.h"
+#include "conv_loader.h"
+
+#ifndef SPK_FEXP
+#define SPK_FEXP 0   // ablation builds only (tools/fexp.sh), bit mask: 1 no MFMA, 2 no in-loop A loads,
+                     // 4 no in-loop A split / stores, 8 no in-loop B DMA, 16 no epilogue stores
+#endif
+
+namespace spk {
+
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int FBM = 128, FBN = 128, FBK = 32, FWM = 2, FWN = 4, FNT = 64 * FWM * FWN;
+constexpr int FTM = FBM / FWM / 32;                  // 32x32 tiles per wave along M (2)
+constexpr int F_LROW = FBK + 8;                      // A rows: 32 halves + 8 (conflict-free b128)
+constexpr int F_PA = FBM * F_LROW;                   // halves per A plane
+constexpr int F_ASTAGE = 2 * F_PA * 2;               // bytes: A hi + lo
+constexpr int F_CHUNKS = (FBN / 32) * 2 * 2;         // B chunks per K-tile: n-tiles x k-steps x planes
+constexpr int F_BSTAGE = F_CHUNKS * 1024;            // bytes
+constexpr int F_STAGE = F_ASTAGE + F_BSTAGE;         // 36864 B
+constexpr int F_LDS_BYTES = 2 * F_STAGE;             // double buffer: 73728 B (two blocks per CU)
+constexpr int F_EPI_BYTES = FWM * FWN * FTM * 1024 * 4;
+static_assert(F_EPI_BYTES <= F_LDS_BYTES, "epilogue slab must fit the staging LDS");
+constexpr int F_ROWS = FBM / (FNT / 8);              // A rows staged per thread (2)
+
+// LDS-DMA of one 16-B slot per lane: LDS[m0_base + 16 lane] = mem[rsrc + voff + soff].
+// M0 is compiler-reserved: saved and restored inside the statement.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %4\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(soff), "s"(lds_base)
+      : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
+}
+
+template <bool ADD>
+__global__ void __launch_bounds__(FNT, 4)
+conv_gemm_x3f_kernel(const ConvDesc d) {
+  SPK_GATE(d.run_if);
+  __shared__ __attribute__((aligned(16))) float lds[F_LDS_BYTES / 4];
+  char* const lb = reinterpret_cast<char*>(lds);
+  const uint32_t lbase = lds_addr(lb);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / FWN, wn = wave % FWN;
+  const int M = d.nimg * d.Ho * d.Wo;
+  const int nN = (d.N + FBN - 1) / FBN;
+  const int nM = (M + FBM - 1) / FBM;
+  const int lid = xcd_remap(blockIdx.x, nM * nN);
+  const int mt = lid / nN, nt = lid % nN;
+  const int m0 = mt * FBM, n0 = nt * FBN;
+
+  const int nkt_all = d.Kp / FBK;
+  const int per = (nkt_all + d.ksplit - 1) / d.ksplit;
+  const int kt0 = blockIdx.z * per;
+  const int kt1 = min(nkt_all, kt0 + per);
+
+  // ---- A: per-row constants (conv_loader.h BufALoader, without the reflect / kcb forms)
+  const int kq = tid & 7, row0 = tid >> 3;            // thread: quad kq of rows row0, row0 + 64
+  const int img0 = m0 / (d.Ho * d.Wo);
+  const size_t img_px = (size_t)d.s0.H * d.s0.W;
+  const __amdgpu_buffer_rsrc_t r0 = make_rsrc(d.s0.p + (size_t)img0 * img_px * d.s0.ld);
+  __amdgpu_buffer_rsrc_t r2;
+  if (ADD) r2 = make_rsrc(d.s0.p2 + (size_t)img0 * img_px * d.s0.ld2);
+  uint32_t roff[F_ROWS], roff2[ADD ? F_ROWS : 1], rmask[F_ROWS];
+#pragma unroll
+  for (int r = 0; r < F_ROWS; ++r) {
+    const int m = m0 + row0 + 64 * r;
+    const bool valid = m < M;
+    const int mm = valid ? m : m0;
+    const int wo = mm % d.Wo, t2 = mm / d.Wo, ho = t2 % d.Ho, img = t2 / d.Ho;
+    const int hb = ho * d.s0.sh - d.s0.ph, wb = wo * d.s0.sw - d.s0.pw;
+    const int pix = ((img - img0) * d.s0.H + hb) * d.s0.W + wb;   // may be negative: masked
+    roff[r] = (uint32_t)pix * (uint32_t)d.s0.ld * 4u;
+    if (ADD) roff2[r] = (uint32_t)pix * (uint32_t)d.s0.ld2 * 4u;
+    const int wl = d.s0.vlen ? min(d.s0.W, d.s0.vlen[img]) : d.s0.W;
+    uint32_t mk = 0;
+    for (int ky = 0; ky < d.s0.kh; ++ky) {
+      const int hi = hb + ky * d.s0.dh;
+      if (hi < 0 || hi >= d.s0.H) continue;
+      for (int x = 0; x < d.s0.kw; ++x) {
+        const int wi = wb + x * d.s0.dw;
+        if (wi >= 0 && wi < wl) mk |= 1u << (ky * d.s0.kw + x);
+      }
+    }
+    rmask[r] = valid ? mk : 0u;   // bit `taps` (K padding past the last tap) is never set
+  }
+
+  // ---- scalar K walk: tile start (tap t0, channel c0), pixel deltas of taps t0 and t0 + 1
+  const int cin = d.s0.cin, kw = d.s0.kw;
+  const int dyW = d.s0.dh * d.s0.W, dx = d.s0.dw;
+  int t0, c0, kyB, kxB, tdpA, tdpB;
+  {
+    const int k = kt0 * FBK;
+    t0 = k / cin;
+    c0 = k - t0 * cin;
+    const int ky = t0 / kw, kx = t0 - ky * kw;
+    tdpA = ky * dyW + kx * dx;
+    kxB = kx + 1;
+    kyB = ky;
+    if (kxB == kw) { kxB = 0; ++kyB; }
+    tdpB = kyB * dyW + kxB * dx;
+  }
+
+  // ---- B: this wave's two DMA chunks of a K-tile (chunk cb = 2 wave + j of the block's 16)
+  const int NJ = nN * (FBN / 32);                      // 32-column n-tiles of the packed matrix
+  const __amdgpu_buffer_rsrc_t brs = make_rsrc(d.wf);
+  const uint32_t bvoff = (uint32_t)lane * 16u;
+  auto dma_b = [&](int kt, int buf) {
+    if ((SPK_FEXP & 8) && kt != kt0) return;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int cb = 2 * wave + j;
+      const uint32_t soff = (uint32_t)(((kt * NJ + nt * (FBN / 32)) * 4 + cb) * 1024);
+      dma16(brs, bvoff, __builtin_amdgcn_readfirstlane(soff),
+            __builtin_amdgcn_readfirstlane(lbase + buf * F_STAGE + F_ASTAGE + cb * 1024));
+    }
+  };
+
+  struct ASet {
+    f32x4 v[F_ROWS];
+    f32x4 v2[ADD ? F_ROWS : 1];
+  };
+  // issue the A loads of the K-tile at the walk position, then advance the walk by BK
+  bool inloop = false;   // (ablation builds)
+  auto load_a = [&](ASet& s) {
+    const int c = c0 + 4 * kq;
+    const bool sel = c >= cin;                         // this quad lies in tap t0 + 1
+    const int cc = sel ? c - cin : c;
+    const int t = min(t0 + (sel ? 1 : 0), 31);       // past the last tap (K padding): no mask bit
+    const int tdp = sel ? tdpB : tdpA;
+    const uint32_t toff = (uint32_t)(tdp * d.s0.ld + cc) * 4u;
+    const uint32_t toff2 = ADD ? (uint32_t)(tdp * d.s0.ld2 + cc) * 4u : 0u;
+#pragma unroll
+    for (int r = 0; r < F_ROWS; ++r) {
+      const bool ok = (rmask[r] >> t) & 1u;
+      if (!(SPK_FEXP & 2) || !inloop) {
+        s.v[r] = buf_load4(r0, ok ? roff[r] + toff : BUF_OOB);
+        if (ADD) s.v2[r] = buf_load4(r2, ok ? roff2[r] + toff2 : BUF_OOB);
+      }
+    }
+    c0 += FBK;
+    if (c0 >= cin) {                                   // cin >= 32: one tap boundary per K-tile
+      c0 -= cin;
+      ++t0;
+      tdpA = tdpB;
+      if (++kxB == kw) { kxB = 0; ++kyB; }
+      tdpB = kyB * dyW + kxB * dx;
+    }
+  };
+  auto store_a = [&](int buf, const ASet& s) {
+    if ((SPK_FEXP & 4) && inloop) return;
+    _Float16* ahi = reinterpret_cast<_Float16*>(lb + buf * F_STAGE);
+    _Float16* alo = ahi + F_PA;
+#pragma unroll
+    for (int r = 0; r < F_ROWS; ++r) {
+      f32x4 v = s.v[r];
+      if (ADD) v += s.v2[r];
+      f16x4 h, l;
+      split_x3(v, h, l);
+      const int off = (row0 + 64 * r) * F_LROW + kq * 4;
+      *reinterpret_cast<f16x4*>(ahi + off) = h;
+      *reinterpret_cast<f16x4*>(alo + off) = l;
+    }
+  };
+
+  f32x16 acc[FTM][1];
+#pragma unroll
+  for (int i = 0; i < FTM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][0][r] = 0.f;
+
+  const int li = lane & 31, lh = lane >> 5;
+  auto compute = [&](int buf) {
+    const _Float16* ahi = reinterpret_cast<const _Float16*>(lb + buf * F_STAGE);
+    const char* bb = lb + buf * F_STAGE + F_ASTAGE + wn * 4096 + lane * 16;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      f16x8 ah[FTM], al[FTM];
+#pragma unroll
+      for (int i = 0; i < FTM; ++i) {
+        const _Float16* p = ahi + (wm * 64 + i * 32 + li) * F_LROW + lh * 16 + 8 * s;
+        ah[i] = *reinterpret_cast<const f16x8*>(p);
+        al[i] = *reinterpret_cast<const f16x8*>(p + F_PA);
+      }
+      const f16x8 bh = *reinterpret_cast<const f16x8*>(bb + s * 2048);
+      const f16x8 bl = *reinterpret_cast<const f16x8*>(bb + s * 2048 + 1024);
+      const f16x8 bh2 = bh * (_Float16)2048.0f;   // exact (|w| < 31.5: ConvDesc::wbig)
+#pragma unroll
+      for (int i = 0; i < FTM; ++i) {
+        if (SPK_FEXP & 1) {
+          acc[i][0][0] += (float)ah[i][0] + (float)bh2[1] + (float)bl[2] + (float)al[i][3] + (float)bh[4];
+          continue;
+        }
+        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh2, acc[i][0], 0, 0, 0);
+        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl, acc[i][0], 0, 0, 0);
+        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh, acc[i][0], 0, 0, 0);
+      }
+    }
+  };
+
+  constexpr int ALOADS = F_ROWS * (ADD ? 2 : 1);     // ordinary loads per A set
+  // Pairs of K-tiles (even step: LDS buffer 0, odd step: buffer 1; A register sets 0 / 1 two
+  // K-tiles ahead), an odd last K-tile peeled after the loop: the loop has one back edge, so
+  // hipcc's wait counting sees the same loads in flight on both paths into its header (with a
+  // `break` between the steps it merged two states and waited vmcnt(0) at the top).  Every
+  // load and DMA in the loop is unconditional (clamped past the end: zeros, or a re-read of
+  // the last tile into the idle buffer), so the body has no branch around a memory operation.
+  if (kt0 < kt1) {
+    ASet set0, set1;
+    dma_b(kt0, 0);
+    load_a(set0);
+    load_a(set1);                                      // kt0 + 1 (or past the end: unused)
+    store_a(0, set0);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALOADS) : "memory");   // B of kt0 landed
+    __syncthreads();
+    inloop = true;
+    int kt = kt0;
+    for (; kt + 1 < kt1; kt += 2) {
+      // even step: buffer 0 holds kt; set 1 holds kt + 1 (in flight)
+      dma_b(kt + 1, 1);
+      load_a(set0);                                    // kt + 2
+      compute(0);
+      store_a(1, set1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALOADS) : "memory");   // B of kt + 1 landed
+      __syncthreads();
+      // odd step: buffer 1 holds kt + 1; set 0 holds kt + 2 (in flight)
+      dma_b(min(kt + 2, kt1 - 1), 0);
+      load_a(set1);                                    // kt + 3
+      compute(1);
+      store_a(0, set0);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALOADS) : "memory");
+      __syncthreads();
+    }
+    if (kt < kt1) {                                    // odd count: the last K-tile is in buffer 0
+      compute(0);
+      __syncthreads();                                 // the epilogue reuses the LDS
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < FTM; ++i) acc[i][0] *= (1.0f / 2048.0f);
+#if SPK_FEXP & 16
+  if (acc[0][0][0] == 1234.5f && acc[1][0][3] == 77.f) d.out[tid] = acc[0][0][1];
+#else
+  epilogue_tiles<FTM, 1>(d, lds, acc, wave, lane, n0 + wn * 32, M, [&](int r) { return m0 + wm * 64 + r; });
+#endif
+}
+
+// fragment order of one packed weight matrix (see the file comment):
+// out[((kt * NJ + j) * 4 + s * 2 + p) * 512 + lane * 8 + e] = plane_p[n][k] with
+// n = 32 j + (lane & 31), k = 32 kt + 16 (lane >> 5) + 8 s + e (zero for n >= N)
+__global__ void pack_frag_kernel(const uint16_t* __restrict__ wh, const uint16_t* __restrict__ wl, int N, int Kp,
+                                 int NJ, uint16_t* __restrict__ out) {
+  const size_t total = (size_t)(Kp / 32) * NJ * 4 * 64;   // 16-B slots
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(i & 63);
+    const size_t ch = i >> 6;
+    const int p = (int)(ch & 1), s = (int)((ch >> 1) & 1);
+    const size_t kj = ch >> 2;
+    const int j = (int)(kj % NJ), kt = (int)(kj / NJ);
+    const int n = 32 * j + (lane & 31), k = 32 * kt + 16 * (lane >> 5) + 8 * s;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (n < N) v = *reinterpret_cast<const u32x4*>((p ? wl : wh) + (size_t)n * Kp + k);
+    *reinterpret_cast<u32x4*>(out + i * 8) = v;
+  }
+}
+
+}  // namespace
+
+size_t frag_halves(int N, int Kp) { return (size_t)Kp * (size_t)((N + FBN - 1) / FBN * FBN) * 2; }
+
+hipError_t launch_pack_frag(const uint16_t* wh, const uint16_t* wl, int N, int Kp, uint16_t* out, hipStream_t s) {
+  if (N <= 0 || Kp <= 0 || Kp % 32 || !wh || !wl || !out) return hipErrorInvalidValue;
+  const int NJ = (N + FBN - 1) / FBN * (FBN / 32);
+  const size_t slots = (size_t)(Kp / 32) * NJ * 256;
+  const int blocks = (int)std::min<size_t>((slots + 255) / 256, 4096);
+  hipLaunchKernelGGL(pack_frag_kernel, dim3(blocks), dim3(256), 0, s, wh, wl, N, Kp, NJ, out);
+  return hipGetLastError();
+}
+
+bool gemm_f_supported(const ConvDesc& d) {
+  static const bool off = [] {
+    const char* e = std::getenv("SPK_GEMM_F");
+    return e && std::string(e) == "0";
+  }();
+  const int M = d.nimg * d.Ho * d.Wo;
+  return !off && d.wf && d.wh && d.wl && !d.wbig && !d.x1 && !d.kcb && !d.s0.reflect && !d.s0.pre_scale &&
+         !d.s1.p && d.s1.cin == 0 && d.N > 64 && M > 4096 && d.Kp % FBK == 0 && d.Kp >= d.K &&
+         conv_buf_loader_ok(d, FBM);
+}
+
+std::string gemm_f_kernel_name(const ConvDesc& d) {
+  const bool add = d.s0.p2 != nullptr || d.s0.ld2 > 0;
+  return std::string("conv_gemm_x3f_kernel<") + (add ? "true" : "false") + ">";
+}
+
+hipError_t launch_gemm_f(const ConvDesc& d, hipStream_t s) {
+  if (!gemm_f_supported(d)) return hipErrorInvalidValue;
+  const int M = d.nimg * d.Ho * d.Wo;
+  const int nblk = ((M + FBM - 1) / FBM) * ((d.N + FBN - 1) / FBN);
+  dim3 grid(nblk, 1, d.ksplit);
+  if (d.s0.p2) hipLaunchKernelGGL(conv_gemm_x3f_kernel<true>, grid, dim3(FNT), 0, s, d);
+  else hipLaunchKernelGGL(conv_gemm_x3f_kernel<false>, grid, dim3(FNT), 0, s, d);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || d.ksplit <= 1) return e;
+  return launch_splitk_reduce(d, s);
+}
+
+}  // namespace spk

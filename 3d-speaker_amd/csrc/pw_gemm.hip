@@ -248,7 +248,9 @@ hipError_t launch_pw_t(const ConvDesc& d, hipStream_t s) {
   return hipGetLastError();
 }
 
-int pw_bn(const ConvDesc& d) { return d.N <= 32 ? 32 : d.N <= 64 ? 64 : 128; }
+// the 32-wide slice exists for Kp == 32 only (SPK_PW(32, 32)); a deeper K with N <= 32 takes
+// the 64-wide slice (its zero columns are masked)
+int pw_bn(const ConvDesc& d) { return d.Kp == 32 ? 32 : d.N <= 64 ? 64 : 128; }
 
 }  // namespace
 

@@ -215,6 +215,7 @@ void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const C
   d.w = m.dptr(p.w_off);
   d.wh = exact ? nullptr : m.dhi(p.w_off);   // no split planes: the exact-fp32 kernels are chosen
   d.wl = exact ? nullptr : m.dlo(p.w_off);
+  d.wf = (exact || !m.dfrag || p.f_off == SIZE_MAX) ? nullptr : m.dfrag + p.f_off;
   const bool guard = !exact;   // producers note fp16x3 range overflows in the forward's word
   d.x1 = (!exact && m.fp16 && x1_scope) ? 1 : 0;
   d.wbig = p.wmax >= kX3WeightLimit ? 1 : 0;
@@ -301,13 +302,39 @@ int hip_check(hipError_t e, const char* what) {
 
 }  // namespace
 
-bool spk::PlanPair::idle() const { return !last || hipEventQuery(last) == hipSuccess; }
+bool spk::PlanPair::idle() const {
+  for (const auto& e : last)
+    if (hipEventQuery(e.second) != hipSuccess) return false;
+  return true;
+}
+
+hipError_t spk::PlanPair::mark(hipStream_t s) {
+  // one event per stream; an entry whose replay has completed is reused for a new stream, so
+  // the list stays as long as the number of streams with a replay in flight
+  hipEvent_t* ev = nullptr;
+  for (auto& e : last)
+    if (e.first == s) ev = &e.second;
+  if (!ev)
+    for (auto& e : last)
+      if (hipEventQuery(e.second) == hipSuccess) {
+        e.first = s;
+        ev = &e.second;
+        break;
+      }
+  if (!ev) {
+    hipEvent_t e = nullptr;
+    if (hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming); r != hipSuccess) return r;
+    last.emplace_back(s, e);
+    ev = &last.back().second;
+  }
+  return hipEventRecord(*ev, s);
+}
 
 spk::PlanPair::~PlanPair() {
   // reached only for an idle pair (Model::retired sweep, handle destruction): no device-wide
   // synchronisation here, which would stall every stream and break a caller's stream capture
   for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
-  if (last) (void)hipEventDestroy(last);
+  for (auto& e : last) (void)hipEventDestroy(e.second);
 }
 
 namespace {
@@ -508,6 +535,23 @@ int spk_model_create(const spk_model_config_t* cfg, const spk_weight_t* weights,
       if (int rc = hip_check(launch_split_f16(h->m.dweights, h->m.dsplit, h->m.dsplit + n, n, nullptr),
                              "split_f16"))
         return rc;
+      // the same planes in MFMA fragment order for the LDS-DMA GEMM (conv_gemm_f.hip): every
+      // matrix wide enough for its 128-column tiles
+      size_t fh = 0;
+      for (auto& kv : h->m.packed)
+        if (kv.second.N > 64 && kv.second.Kp > 0 && kv.second.Kp % 32 == 0) {
+          kv.second.f_off = fh;
+          fh += frag_halves(kv.second.N, kv.second.Kp);
+        }
+      if (fh) {
+        if (int rc = hip_check(hipMalloc(&h->m.dfrag, fh * sizeof(uint16_t)), "hipMalloc(fragment weights)")) return rc;
+        for (auto& kv : h->m.packed)
+          if (kv.second.f_off != SIZE_MAX)
+            if (int rc = hip_check(launch_pack_frag(h->m.dhi(kv.second.w_off), h->m.dlo(kv.second.w_off), kv.second.N,
+                                                    kv.second.Kp, h->m.dfrag + kv.second.f_off, nullptr),
+                                   "pack_frag"))
+              return rc;
+      }
       if (int rc = hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize")) return rc;
     }
     {
@@ -534,6 +578,7 @@ int spk_model_destroy(spk_model_t* model) {
   if (busy) (void)hipDeviceSynchronize();
   if (model->m.dweights) (void)hipFree(model->m.dweights);
   if (model->m.dsplit) (void)hipFree(model->m.dsplit);
+  if (model->m.dfrag) (void)hipFree(model->m.dfrag);
   delete model;
   return SPK_OK;
 }
@@ -690,12 +735,11 @@ static int run_graph(const char* fn, spk_model_t* model, PlanPair& pp, const flo
   if (int rc = hip_check(hipGraphLaunch(exec, stream), "hipGraphLaunch")) return rc;
   if (int rc = hip_check(hipMemcpyAsync(emb_out, out_s, pp.out_bytes, hipMemcpyDeviceToDevice, stream), "stage out"))
     return rc;
-  // completion marker of this replay (PlanPair::last): an evicted pair is freed only after it
+  // completion marker of this replay on this stream (PlanPair::last): an evicted pair is
+  // freed only after the replays on every stream are done
   {
     std::lock_guard<std::mutex> lk(model->m.mu);
-    if (!pp.last)
-      if (int rc = hip_check(hipEventCreateWithFlags(&pp.last, hipEventDisableTiming), "hipEventCreate")) return rc;
-    return hip_check(hipEventRecord(pp.last, stream), "hipEventRecord");
+    return hip_check(pp.mark(stream), "hipEventRecord");
   }
 }
 

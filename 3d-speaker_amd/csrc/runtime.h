@@ -77,11 +77,14 @@ struct PlanPair {
   size_t stage_in = 0, stage_out = 0, stage_len = 0, stage_flag = 0;
   size_t in_bytes = 0, out_bytes = 0, len_bytes = 0;
   std::map<const void*, hipGraphExec_t> graphs;
-  // completion of the last graph replay enqueued from this pair (recorded on the caller's
-  // stream after the launch): an evicted pair's executable graphs are destroyed only once it
-  // has completed (Model::retired), never by synchronising the device
-  hipEvent_t last = nullptr;
-  bool idle() const;                // no replay of this pair can still be running
+  // completion of the last graph replay enqueued from this pair on each stream it was
+  // replayed on (recorded after the launch; a pair's graphs can be replayed from several
+  // threads on several streams): an evicted pair's executable graphs are destroyed only once
+  // every one of them has completed (Model::retired), never by synchronising the device.
+  // Guarded by Model::mu.
+  std::vector<std::pair<hipStream_t, hipEvent_t>> last;
+  bool idle() const;                // no replay of this pair can still be running, on any stream
+  hipError_t mark(hipStream_t s);   // record this stream's completion event behind a replay
   ~PlanPair();
 };
 
@@ -104,6 +107,7 @@ struct Packed {
   double l1max = 0.0;                             // max over output channels of sum_k |w| (bounds)
   double bmax = 0.0;                              // max |bias|
   int kcb = 0;                                    // K order (common.h ConvDesc::kcb)
+  size_t f_off = SIZE_MAX;                        // fragment-order copy in Model::dfrag (halves)
 };
 
 // One weight tensor's contribution to a packed GEMM.
@@ -127,6 +131,7 @@ struct Model {
   float* dweights = nullptr;
   size_t dweights_bytes = 0;
   uint16_t* dsplit = nullptr;                     // fp16 hi plane then lo plane of the whole arena
+  uint16_t* dfrag = nullptr;                      // MFMA fragment order of the LDS-DMA GEMM's weights
   std::map<std::string, Packed> packed;
   // launch plans by (B, T, ragged): the fp16x3 plan and its exact-fp32 twin (the range
   // guard's gated re-run; the same object when the handle runs exact only), sharing one

@@ -418,7 +418,9 @@ hipError_t launch_cam_gate(const float* x, int B, int T, int C, int ld, int seg,
   hipLaunchKernelGGL(cam_segsum_kernel, dim3(nseg, B), dim3(256), 0, s, x, T, C, ld, seg, nseg, segsum, vlen, launch_gate());
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   static const bool lean_off = std::getenv("SPK_CAM_GATE_LDS") != nullptr;   // A/B: the transposing kernel
-  const bool lean = !lean_off && 256 % red == 0 && 256 % growth == 0 && C % (4 * (256 / red)) == 0 &&
+  // the lean kernel's butterfly sums Q = 256 / red (or 256 / growth) adjacent lanes with
+  // __shfl_xor, i.e. within one wave only when Q <= 64
+  const bool lean = !lean_off && red >= 4 && growth >= 4 && 256 % red == 0 && 256 % growth == 0 && C % (4 * (256 / red)) == 0 &&
                     red % (4 * (256 / growth)) == 0 && C / (256 / red) <= 4 * CAM_WQ &&
                     red / (256 / growth) <= 4 * CAM_WQ && k1p % 4 == 0 && k2p % 4 == 0 &&
                     (reinterpret_cast<uintptr_t>(w1) & 15) == 0 && (reinterpret_cast<uintptr_t>(w2) & 15) == 0;

@@ -463,7 +463,13 @@ def main(argv=None):
     ngpus = torch.cuda.device_count()
     if ngpus == 0:
         raise RuntimeError('[ERROR]: no ROCm device: the MI355X build has no CPU inference path')
-    nprocs = (args.nprocs or ngpus) if args.shard_chunks else min(len(wav_list), args.nprocs or ngpus)
+    if args.shard_chunks:
+        # one rank per GPU: RCCL refuses two ranks of one process group on the same device
+        nprocs = min(args.nprocs or ngpus, ngpus)
+        if args.nprocs and args.nprocs > ngpus:
+            print(f'[WARNING]: --shard_chunks runs one rank per GPU: --nprocs {args.nprocs} capped at {ngpus}.')
+    else:
+        nprocs = min(len(wav_list), args.nprocs or ngpus)
     print(f'[INFO]: Set {nprocs} processes to extract embeddings.')
     if args.out_dir is not None:
         os.makedirs(args.out_dir, exist_ok=True)

@@ -139,6 +139,9 @@ hipError_t launch_aff_x3(const AffDesc& a, hipStream_t) {
 // the emulated GEMM reads the fp32 weights; the split planes are not needed on the host
 hipError_t launch_split_f16(const float*, uint16_t*, uint16_t*, size_t, hipStream_t) {
   EMU_GATE(); return hipSuccess; }
+// nor the fragment-order copy of the LDS-DMA GEMM (conv_gemm_f.hip)
+size_t frag_halves(int N, int Kp) { return (size_t)Kp * (size_t)((N + 127) / 128 * 128) * 2; }
+hipError_t launch_pack_frag(const uint16_t*, const uint16_t*, int, int, uint16_t*, hipStream_t) { return hipSuccess; }
 
 static void emu_range_note(int* flag, float v) {   // common.h range guard
   if (flag && std::fabs(v) >= kRangeLimit) *flag |= 1;
