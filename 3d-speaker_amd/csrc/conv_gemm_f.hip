@@ -26,6 +26,7 @@
 // products, same K order): x w ~= 2^-11 (hi_x (2^11 hi_w) + hi_x lo_w + lo_x hi_w).
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #include "common.h"
 #include "conv_epilogue.h"
@@ -44,18 +45,32 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int FBM = 128, FBN = 128, FBK = 32, FWM = 2, FWN = 4, FNT = 64 * FWM * FWN;
-constexpr int FTM = FBM / FWM / 32;                  // 32x32 tiles per wave along M (2)
-constexpr int F_LROW = FBK + 8;                      // A rows: 32 halves + 8 (conflict-free b128)
-constexpr int F_PA = FBM * F_LROW;                   // halves per A plane
-constexpr int F_ASTAGE = 2 * F_PA * 2;               // bytes: A hi + lo
-constexpr int F_CHUNKS = (FBN / 32) * 2 * 2;         // B chunks per K-tile: n-tiles x k-steps x planes
-constexpr int F_BSTAGE = F_CHUNKS * 1024;            // bytes
-constexpr int F_STAGE = F_ASTAGE + F_BSTAGE;         // 36864 B
-constexpr int F_LDS_BYTES = 2 * F_STAGE;             // double buffer: 73728 B (two blocks per CU)
-constexpr int F_EPI_BYTES = FWM * FWN * FTM * 1024 * 4;
-static_assert(F_EPI_BYTES <= F_LDS_BYTES, "epilogue slab must fit the staging LDS");
-constexpr int F_ROWS = FBM / (FNT / 8);              // A rows staged per thread (2)
+constexpr int FBK = 32;
+constexpr int F_NPAD = 256;                          // packed N padded to the widest tile
+
+// Tile geometry: BM x BN block tile, WM x WN waves, each wave TM x TN 32x32 accumulator tiles.
+template <int BM, int BN, int WM, int WN>
+struct FCfg {
+  static constexpr int NT = 64 * WM * WN;
+  static constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  static constexpr int LROW = FBK + 8;               // A rows: 32 halves + 8 (conflict-free b128)
+  static constexpr int PA = BM * LROW;               // halves per A plane
+  static constexpr int ASTAGE = 2 * PA * 2;          // bytes: A hi + lo
+  static constexpr int CHUNKS = (BN / 32) * 2 * 2;   // B chunks per K-tile: n-tiles x k-steps x planes
+  static constexpr int CPW = CHUNKS / (WM * WN);     // DMA chunks per wave per K-tile
+  static constexpr int STAGE = ASTAGE + CHUNKS * 1024;
+  // epilogue_tiles' slab: the whole wave tile when it fits next to nothing else (128 x 128),
+  // else one row of accumulator tiles at a time
+  static constexpr int EPI_ALL = WM * WN * TM * TN * 1024 * 4;
+  static constexpr bool EPI_ONE = EPI_ALL <= 2 * STAGE;
+  static constexpr int EPI = EPI_ONE ? EPI_ALL : WM * WN * TN * 1024 * 4;
+  static constexpr int LDS = 2 * STAGE > EPI ? 2 * STAGE : EPI;
+  static constexpr int ROWS = BM / (NT / 8);         // A rows staged per thread
+  static constexpr bool ONE_SET = TM * TN >= 8;     // 128 accumulator registers per wave
+  static constexpr int WAVES_PER_EU = LDS <= 80 * 1024 ? 2 * WM * WN / 4 : WM * WN / 4;
+  static_assert(TM >= 1 && TN >= 1 && CPW >= 1 && CHUNKS % (WM * WN) == 0 && BM % (NT / 8) == 0, "tile");
+  static_assert(LDS <= 160 * 1024, "LDS");
+};
 
 // LDS-DMA of one 16-B slot per lane: LDS[m0_base + 16 lane] = mem[rsrc + voff + soff].
 // M0 is compiler-reserved: saved and restored inside the statement.
@@ -72,27 +87,44 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, 
       : "memory");
 }
 
+template <int I, int E>
+struct StaticFor {
+  template <class F>
+  __device__ __forceinline__ static void run(F& f) {
+    f(std::integral_constant<int, I>{});
+    StaticFor<I + 1, E>::run(f);
+  }
+};
+template <int E>
+struct StaticFor<E, E> {
+  template <class F>
+  __device__ __forceinline__ static void run(F&) {}
+};
+
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
 }
 
-template <bool ADD>
-__global__ void __launch_bounds__(FNT, 4)
+template <int BM, int BN, int WM, int WN, bool ADD>
+__global__ void __launch_bounds__(64 * WM * WN, (FCfg<BM, BN, WM, WN>::WAVES_PER_EU))
 conv_gemm_x3f_kernel(const ConvDesc d) {
   SPK_GATE(d.run_if);
-  __shared__ __attribute__((aligned(16))) float lds[F_LDS_BYTES / 4];
+  using C = FCfg<BM, BN, WM, WN>;
+  constexpr int TM = C::TM, TN = C::TN, ROWS = C::ROWS, NT = C::NT;
+  constexpr int RPP = NT / 8;                          // rows per staging pass
+  __shared__ __attribute__((aligned(16))) float lds[C::LDS / 4];
   char* const lb = reinterpret_cast<char*>(lds);
   const uint32_t lbase = lds_addr(lb);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / FWN, wn = wave % FWN;
+  const int wm = wave / WN, wn = wave % WN;
   const int M = d.nimg * d.Ho * d.Wo;
-  const int nN = (d.N + FBN - 1) / FBN;
-  const int nM = (M + FBM - 1) / FBM;
+  const int nN = (d.N + BN - 1) / BN;
+  const int nM = (M + BM - 1) / BM;
   const int lid = xcd_remap(blockIdx.x, nM * nN);
   const int mt = lid / nN, nt = lid % nN;
-  const int m0 = mt * FBM, n0 = nt * FBN;
+  const int m0 = mt * BM, n0 = nt * BN;
 
   const int nkt_all = d.Kp / FBK;
   const int per = (nkt_all + d.ksplit - 1) / d.ksplit;
@@ -100,16 +132,16 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
   const int kt1 = min(nkt_all, kt0 + per);
 
   // ---- A: per-row constants (conv_loader.h BufALoader, without the reflect / kcb forms)
-  const int kq = tid & 7, row0 = tid >> 3;            // thread: quad kq of rows row0, row0 + 64
+  const int kq = tid & 7, row0 = tid >> 3;            // thread: quad kq of rows row0 + RPP r
   const int img0 = m0 / (d.Ho * d.Wo);
   const size_t img_px = (size_t)d.s0.H * d.s0.W;
   const __amdgpu_buffer_rsrc_t r0 = make_rsrc(d.s0.p + (size_t)img0 * img_px * d.s0.ld);
   __amdgpu_buffer_rsrc_t r2;
   if (ADD) r2 = make_rsrc(d.s0.p2 + (size_t)img0 * img_px * d.s0.ld2);
-  uint32_t roff[F_ROWS], roff2[ADD ? F_ROWS : 1], rmask[F_ROWS];
+  uint32_t roff[ROWS], roff2[ADD ? ROWS : 1], rmask[ROWS];
 #pragma unroll
-  for (int r = 0; r < F_ROWS; ++r) {
-    const int m = m0 + row0 + 64 * r;
+  for (int r = 0; r < ROWS; ++r) {
+    const int m = m0 + row0 + RPP * r;
     const bool valid = m < M;
     const int mm = valid ? m : m0;
     const int wo = mm % d.Wo, t2 = mm / d.Wo, ho = t2 % d.Ho, img = t2 / d.Ho;
@@ -146,24 +178,25 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
     tdpB = kyB * dyW + kxB * dx;
   }
 
-  // ---- B: this wave's two DMA chunks of a K-tile (chunk cb = 2 wave + j of the block's 16)
-  const int NJ = nN * (FBN / 32);                      // 32-column n-tiles of the packed matrix
+  // ---- B: this wave's DMA chunks of a K-tile (chunk cb = CPW wave + j of the block's CHUNKS,
+  // cb = (local n-tile) * 4 + k-step * 2 + plane)
+  const int NJ = (d.N + F_NPAD - 1) / F_NPAD * (F_NPAD / 32);   // 32-column n-tiles of the packed matrix
   const __amdgpu_buffer_rsrc_t brs = make_rsrc(d.wf);
   const uint32_t bvoff = (uint32_t)lane * 16u;
   auto dma_b = [&](int kt, int buf) {
     if ((SPK_FEXP & 8) && kt != kt0) return;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int cb = 2 * wave + j;
-      const uint32_t soff = (uint32_t)(((kt * NJ + nt * (FBN / 32)) * 4 + cb) * 1024);
+    for (int j = 0; j < C::CPW; ++j) {
+      const int cb = C::CPW * wave + j;
+      const uint32_t soff = (uint32_t)(((kt * NJ + nt * (BN / 32)) * 4 + cb) * 1024);
       dma16(brs, bvoff, __builtin_amdgcn_readfirstlane(soff),
-            __builtin_amdgcn_readfirstlane(lbase + buf * F_STAGE + F_ASTAGE + cb * 1024));
+            __builtin_amdgcn_readfirstlane(lbase + buf * C::STAGE + C::ASTAGE + cb * 1024));
     }
   };
 
   struct ASet {
-    f32x4 v[F_ROWS];
-    f32x4 v2[ADD ? F_ROWS : 1];
+    f32x4 v[ROWS];
+    f32x4 v2[ADD ? ROWS : 1];
   };
   // issue the A loads of the K-tile at the walk position, then advance the walk by BK
   bool inloop = false;   // (ablation builds)
@@ -176,7 +209,7 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
     const uint32_t toff = (uint32_t)(tdp * d.s0.ld + cc) * 4u;
     const uint32_t toff2 = ADD ? (uint32_t)(tdp * d.s0.ld2 + cc) * 4u : 0u;
 #pragma unroll
-    for (int r = 0; r < F_ROWS; ++r) {
+    for (int r = 0; r < ROWS; ++r) {
       const bool ok = (rmask[r] >> t) & 1u;
       if (!(SPK_FEXP & 2) || !inloop) {
         s.v[r] = buf_load4(r0, ok ? roff[r] + toff : BUF_OOB);
@@ -194,63 +227,94 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
   };
   auto store_a = [&](int buf, const ASet& s) {
     if ((SPK_FEXP & 4) && inloop) return;
-    _Float16* ahi = reinterpret_cast<_Float16*>(lb + buf * F_STAGE);
-    _Float16* alo = ahi + F_PA;
+    _Float16* ahi = reinterpret_cast<_Float16*>(lb + buf * C::STAGE);
+    _Float16* alo = ahi + C::PA;
 #pragma unroll
-    for (int r = 0; r < F_ROWS; ++r) {
+    for (int r = 0; r < ROWS; ++r) {
       f32x4 v = s.v[r];
       if (ADD) v += s.v2[r];
       f16x4 h, l;
       split_x3(v, h, l);
-      const int off = (row0 + 64 * r) * F_LROW + kq * 4;
+      const int off = (row0 + RPP * r) * C::LROW + kq * 4;
       *reinterpret_cast<f16x4*>(ahi + off) = h;
       *reinterpret_cast<f16x4*>(alo + off) = l;
     }
   };
 
-  f32x16 acc[FTM][1];
+  f32x16 acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < FTM; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[i][0][r] = 0.f;
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int li = lane & 31, lh = lane >> 5;
   auto compute = [&](int buf) {
-    const _Float16* ahi = reinterpret_cast<const _Float16*>(lb + buf * F_STAGE);
-    const char* bb = lb + buf * F_STAGE + F_ASTAGE + wn * 4096 + lane * 16;
+    const _Float16* ahi = reinterpret_cast<const _Float16*>(lb + buf * C::STAGE);
+    const char* bb = lb + buf * C::STAGE + C::ASTAGE + wn * TN * 4096 + lane * 16;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      f16x8 ah[FTM], al[FTM];
+      f16x8 ah[TM], al[TM], bh[TN], bl[TN], bh2[TN];
 #pragma unroll
-      for (int i = 0; i < FTM; ++i) {
-        const _Float16* p = ahi + (wm * 64 + i * 32 + li) * F_LROW + lh * 16 + 8 * s;
+      for (int i = 0; i < TM; ++i) {
+        const _Float16* p = ahi + (wm * TM * 32 + i * 32 + li) * C::LROW + lh * 16 + 8 * s;
         ah[i] = *reinterpret_cast<const f16x8*>(p);
-        al[i] = *reinterpret_cast<const f16x8*>(p + F_PA);
+        al[i] = *reinterpret_cast<const f16x8*>(p + C::PA);
       }
-      const f16x8 bh = *reinterpret_cast<const f16x8*>(bb + s * 2048);
-      const f16x8 bl = *reinterpret_cast<const f16x8*>(bb + s * 2048 + 1024);
-      const f16x8 bh2 = bh * (_Float16)2048.0f;   // exact (|w| < 31.5: ConvDesc::wbig)
 #pragma unroll
-      for (int i = 0; i < FTM; ++i) {
-        if (SPK_FEXP & 1) {
-          acc[i][0][0] += (float)ah[i][0] + (float)bh2[1] + (float)bl[2] + (float)al[i][3] + (float)bh[4];
-          continue;
-        }
-        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh2, acc[i][0], 0, 0, 0);
-        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl, acc[i][0], 0, 0, 0);
-        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh, acc[i][0], 0, 0, 0);
+      for (int j = 0; j < TN; ++j) {
+        bh[j] = *reinterpret_cast<const f16x8*>(bb + j * 4096 + s * 2048);
+        bl[j] = *reinterpret_cast<const f16x8*>(bb + j * 4096 + s * 2048 + 1024);
+        bh2[j] = bh[j] * (_Float16)2048.0f;   // exact (|w| < 31.5: ConvDesc::wbig)
       }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if (SPK_FEXP & 1) {
+            acc[i][j][0] += (float)ah[i][0] + (float)bh2[j][1] + (float)bl[j][2] + (float)al[i][3] + (float)bh[j][4];
+            continue;
+          }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh2[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        }
     }
   };
 
-  constexpr int ALOADS = F_ROWS * (ADD ? 2 : 1);     // ordinary loads per A set
+  constexpr int ALOADS = ROWS * (ADD ? 2 : 1);       // ordinary loads per A set
   // Pairs of K-tiles (even step: LDS buffer 0, odd step: buffer 1; A register sets 0 / 1 two
   // K-tiles ahead), an odd last K-tile peeled after the loop: the loop has one back edge, so
   // hipcc's wait counting sees the same loads in flight on both paths into its header (with a
   // `break` between the steps it merged two states and waited vmcnt(0) at the top).  Every
   // load and DMA in the loop is unconditional (clamped past the end: zeros, or a re-read of
   // the last tile into the idle buffer), so the body has no branch around a memory operation.
-  if (kt0 < kt1) {
+  if (C::ONE_SET && kt0 < kt1) {
+    // one A register set (the 256 x 256 tile, whose accumulators take half the registers):
+    // the loads of K-tile kt + 1 are issued right after the stores of kt, so they have the
+    // whole next compute step (48 MFMAs per wave) to land
+    ASet set;
+    dma_b(kt0, 0);
+    load_a(set);
+    store_a(0, set);
+    load_a(set);                                       // kt0 + 1
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALOADS) : "memory");   // B of kt0 landed
+    __syncthreads();
+    inloop = true;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int buf = (kt - kt0) & 1;
+      dma_b(min(kt + 1, kt1 - 1), buf ^ 1);           // buffer buf ^ 1 was read before the last barrier
+      compute(buf);
+      // keep the split of the A set (loaded at the end of the previous step) behind the MFMAs:
+      // hoisted to the top of the step it waited for those loads before any MFMA could issue
+      __builtin_amdgcn_sched_barrier(0);
+      store_a(buf ^ 1, set);                           // K-tile kt + 1 (past the end: unused)
+      load_a(set);                                     // kt + 2
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALOADS) : "memory");   // B of kt + 1 landed
+      __syncthreads();
+    }
+  } else if (kt0 < kt1) {
     ASet set0, set1;
     dma_b(kt0, 0);
     load_a(set0);
@@ -265,6 +329,7 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
       dma_b(kt + 1, 1);
       load_a(set0);                                    // kt + 2
       compute(0);
+      __builtin_amdgcn_sched_barrier(0);
       store_a(1, set1);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALOADS) : "memory");   // B of kt + 1 landed
       __syncthreads();
@@ -272,6 +337,7 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
       dma_b(min(kt + 2, kt1 - 1), 0);
       load_a(set1);                                    // kt + 3
       compute(1);
+      __builtin_amdgcn_sched_barrier(0);
       store_a(0, set0);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALOADS) : "memory");
       __syncthreads();
@@ -282,11 +348,29 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
     }
   }
 #pragma unroll
-  for (int i = 0; i < FTM; ++i) acc[i][0] *= (1.0f / 2048.0f);
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] *= (1.0f / 2048.0f);
 #if SPK_FEXP & 16
-  if (acc[0][0][0] == 1234.5f && acc[1][0][3] == 77.f) d.out[tid] = acc[0][0][1];
+  if (acc[0][0][0] == 1234.5f && acc[TM - 1][TN - 1][3] == 77.f) d.out[tid] = acc[0][0][1];
 #else
-  epilogue_tiles<FTM, 1>(d, lds, acc, wave, lane, n0 + wn * 32, M, [&](int r) { return m0 + wm * 64 + r; });
+  // one row of accumulator tiles at a time through the wave's slab (TN x 4 KB): the whole
+  // wave tile of a 256-wide block would not fit in LDS
+  if constexpr (C::EPI_ONE) {
+    epilogue_tiles<TM, TN>(d, lds, acc, wave, lane, n0 + wn * TN * 32, M, [&](int r) { return m0 + wm * TM * 32 + r; });
+    return;
+  }
+  // compile-time row index (a runtime one, e.g. from a loop the compiler does not unroll around
+  // the large inlined epilogue, puts the accumulators in scratch)
+  auto epi_row = [&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    const int rb = m0 + wm * TM * 32 + i * 32;
+    f32x16 row[1][TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) row[0][j] = acc[i][j];
+    epilogue_tiles<1, TN>(d, lds, row, wave, lane, n0 + wn * TN * 32, M, [&](int r) { return rb + r; });
+  };
+  StaticFor<0, TM>::run(epi_row);
 #endif
 }
 
@@ -311,16 +395,77 @@ __global__ void pack_frag_kernel(const uint16_t* __restrict__ wh, const uint16_t
 
 }  // namespace
 
-size_t frag_halves(int N, int Kp) { return (size_t)Kp * (size_t)((N + FBN - 1) / FBN * FBN) * 2; }
+size_t frag_halves(int N, int Kp) { return (size_t)Kp * (size_t)((N + F_NPAD - 1) / F_NPAD * F_NPAD) * 2; }
 
 hipError_t launch_pack_frag(const uint16_t* wh, const uint16_t* wl, int N, int Kp, uint16_t* out, hipStream_t s) {
   if (N <= 0 || Kp <= 0 || Kp % 32 || !wh || !wl || !out) return hipErrorInvalidValue;
-  const int NJ = (N + FBN - 1) / FBN * (FBN / 32);
+  const int NJ = (N + F_NPAD - 1) / F_NPAD * (F_NPAD / 32);
   const size_t slots = (size_t)(Kp / 32) * NJ * 256;
   const int blocks = (int)std::min<size_t>((slots + 255) / 256, 4096);
   hipLaunchKernelGGL(pack_frag_kernel, dim3(blocks), dim3(256), 0, s, wh, wl, N, Kp, NJ, out);
   return hipGetLastError();
 }
+
+namespace {
+
+struct FTile {
+  int bm, bn;
+};
+
+// tile per layer: SPK_GEMM_F_TILE=128x128 | 256x128 | 128x256 | 256x256 overrides (experiments)
+FTile f_tile(const ConvDesc& d) {
+  static const int forced = [] {
+    const char* e = std::getenv("SPK_GEMM_F_TILE");
+    if (!e) return 0;
+    const std::string v(e);
+    return v == "128x128" ? 1 : v == "256x128" ? 2 : v == "128x256" ? 3 : v == "256x256" ? 4 : 0;
+  }();
+  switch (forced) {
+    case 1: return {128, 128};
+    case 2: return {256, 128};
+    case 3: return {128, 256};
+    case 4: return d.s0.p2 ? FTile{128, 128} : FTile{256, 256};
+    default: break;
+  }
+  // measured (tools/gemm_bench, ERes2NetV2 B = 256 layer shapes, round 5): the 256 x 256 tile
+  // (8 waves of 128 x 64, one block per CU, half the LDS fragment reads per MFMA of the 64 x 32
+  // wave tile) is fastest on every layer with N > 128, even where N = 208 / 416 leaves 19 % of
+  // its columns empty (l3 conv1 313 -> 280 us, l4 conv1 275 -> 230, l4 3x3 215 -> 184, l3_ds
+  // 2067 -> 1766); the 104-wide layers keep 128 x 128 at two blocks per CU
+  // Two conditions keep a layer off it: a last round of blocks that leaves most CUs idle (one
+  // block per CU: ECAPA's 1x1 convs at B = 256, 792 blocks = 3.1 rounds, 0.39 -> 0.55 ms), and
+  // a short K with an epilogue that reads operands (fuse34's AFF conv, K = 256: its epilogue
+  // is not overlapped by a second resident block, 0.22 -> 0.25 ms).
+  const int M = d.nimg * d.Ho * d.Wo;
+  if (d.N > 128 && M >= 16384 && !d.s0.p2 && (d.Kp >= 512 || (!d.res && !d.affx && !d.gate))) {
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0, n = 0;
+      cus = (hipGetDevice(&dev) == hipSuccess &&
+             hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0) ? n : 256;
+    }
+    const double rounds = (double)((M + 255) / 256) * ((d.N + 255) / 256) / cus;
+    const double tail = rounds - (int)rounds;
+    if (rounds >= 4.0 || tail == 0.0 || tail >= 0.6) return {256, 256};
+  }
+  return {128, 128};
+}
+
+template <int BM, int BN, int WM, int WN>
+hipError_t launch_f_t(const ConvDesc& d, hipStream_t s) {
+  const int M = d.nimg * d.Ho * d.Wo;
+  const int nblk = ((M + BM - 1) / BM) * ((d.N + BN - 1) / BN);
+  dim3 grid(nblk, 1, d.ksplit);
+  if (d.s0.p2) {
+    if constexpr (BM * BN >= 256 * 256) return hipErrorInvalidValue;   // f_tile: 128 x 128 for the addend form
+    else hipLaunchKernelGGL((conv_gemm_x3f_kernel<BM, BN, WM, WN, true>), grid, dim3(64 * WM * WN), 0, s, d);
+  } else {
+    hipLaunchKernelGGL((conv_gemm_x3f_kernel<BM, BN, WM, WN, false>), grid, dim3(64 * WM * WN), 0, s, d);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
 
 bool gemm_f_supported(const ConvDesc& d) {
   static const bool off = [] {
@@ -328,24 +473,28 @@ bool gemm_f_supported(const ConvDesc& d) {
     return e && std::string(e) == "0";
   }();
   const int M = d.nimg * d.Ho * d.Wo;
+  const FTile t = f_tile(d);
   return !off && d.wf && d.wh && d.wl && !d.wbig && !d.x1 && !d.kcb && !d.s0.reflect && !d.s0.pre_scale &&
          !d.s1.p && d.s1.cin == 0 && d.N > 64 && M > 4096 && d.Kp % FBK == 0 && d.Kp >= d.K &&
-         conv_buf_loader_ok(d, FBM);
+         conv_buf_loader_ok(d, t.bm);
 }
 
 std::string gemm_f_kernel_name(const ConvDesc& d) {
   const bool add = d.s0.p2 != nullptr || d.s0.ld2 > 0;
-  return std::string("conv_gemm_x3f_kernel<") + (add ? "true" : "false") + ">";
+  const FTile t = f_tile(d);
+  const int wm = t.bm == 256 && t.bn == 128 ? 4 : 2, wn = 8 / wm;
+  return "conv_gemm_x3f_kernel<" + std::to_string(t.bm) + ", " + std::to_string(t.bn) + ", " + std::to_string(wm) +
+         ", " + std::to_string(wn) + ", " + (add ? "true" : "false") + ">";
 }
 
 hipError_t launch_gemm_f(const ConvDesc& d, hipStream_t s) {
   if (!gemm_f_supported(d)) return hipErrorInvalidValue;
-  const int M = d.nimg * d.Ho * d.Wo;
-  const int nblk = ((M + FBM - 1) / FBM) * ((d.N + FBN - 1) / FBN);
-  dim3 grid(nblk, 1, d.ksplit);
-  if (d.s0.p2) hipLaunchKernelGGL(conv_gemm_x3f_kernel<true>, grid, dim3(FNT), 0, s, d);
-  else hipLaunchKernelGGL(conv_gemm_x3f_kernel<false>, grid, dim3(FNT), 0, s, d);
-  hipError_t e = hipGetLastError();
+  const FTile t = f_tile(d);
+  hipError_t e;
+  if (t.bm == 256 && t.bn == 256) e = launch_f_t<256, 256, 2, 4>(d, s);
+  else if (t.bm == 256) e = launch_f_t<256, 128, 4, 2>(d, s);
+  else if (t.bn == 256) e = launch_f_t<128, 256, 2, 4>(d, s);
+  else e = launch_f_t<128, 128, 2, 4>(d, s);
   if (e != hipSuccess || d.ksplit <= 1) return e;
   return launch_splitk_reduce(d, s);
 }

@@ -140,7 +140,7 @@ hipError_t launch_aff_x3(const AffDesc& a, hipStream_t) {
 hipError_t launch_split_f16(const float*, uint16_t*, uint16_t*, size_t, hipStream_t) {
   EMU_GATE(); return hipSuccess; }
 // nor the fragment-order copy of the LDS-DMA GEMM (conv_gemm_f.hip)
-size_t frag_halves(int N, int Kp) { return (size_t)Kp * (size_t)((N + 127) / 128 * 128) * 2; }
+size_t frag_halves(int N, int Kp) { return (size_t)Kp * (size_t)((N + 255) / 256 * 256) * 2; }
 hipError_t launch_pack_frag(const uint16_t*, const uint16_t*, int, int, uint16_t*, hipStream_t) { return hipSuccess; }
 
 static void emu_range_note(int* flag, float v) {   // common.h range guard

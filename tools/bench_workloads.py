@@ -42,11 +42,13 @@ def load(arch, device):
     return helpers.loaded_module(arch).to(device).eval()
 
 
-def c3(args, device):
+def c3_setup(device, precision='fp32', nbuckets=4, n=1024):
+    """The C3 batch and its bucketed forward (also driven by tests/test_gpu_c3_full.py):
+    returns (step, lens, order, host, model); step() gives the embeddings of the utterances in
+    length order, row i = utterance order[i] (waveform host[i, :lens[order[i]]])."""
     from speakerlab import _hip
     from speakerlab.utils import synthetic
     rng = np.random.Generator(np.random.PCG64(2))
-    n = 1024
     lens = rng.integers(16000, 80001, size=n)
     order = np.argsort(lens, kind='stable')
     lens_sorted = lens[order]
@@ -55,8 +57,8 @@ def c3(args, device):
     for i, j in enumerate(order):
         host[i, :lens_sorted[i]] = synthetic.synth_wav(int(lens_sorted[i]), seed=2_000_000 + int(j))
     wavs = torch.from_numpy(host).to(device)
-    model = load('campplus', device).set_hip_precision(args.precision)
-    bounds = np.linspace(0, n, args.buckets + 1).astype(int)
+    model = load('campplus', device).set_hip_precision(precision)
+    bounds = np.linspace(0, n, nbuckets + 1).astype(int)
     buckets = []
     for a, b in zip(bounds[:-1], bounds[1:]):
         lmax = int(lens_sorted[b - 1])
@@ -69,6 +71,12 @@ def c3(args, device):
             outs.append(model(feats, lengths=frames))
         return torch.cat(outs)
 
+    return step, lens, order, host, model
+
+
+def c3(args, device):
+    step, lens, order, host, model = c3_setup(device, args.precision, args.buckets)
+    n = len(lens)
     dt, emb = timed(step, args.steps, args.warmup)
     assert torch.isfinite(emb).all()
     audio_s = float(lens.sum()) / 16000
