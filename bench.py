@@ -96,7 +96,7 @@ def roofline(model, feats, device, traffic_json):
         g['steps'].append((fl, by, ms))
     kern, g = max(groups.items(), key=lambda kv: kv[1]['ms'])
     # fp16x3 kernels: the tiled / persistent x3 GEMMs and the fused Res2Net blocks
-    x3 = '_x3_' in kern or kern.startswith(('res2_block', 'aff_x3'))
+    x3 = '_x3' in kern or kern.startswith(('res2_block', 'aff_x3'))
     peak = PEAK_X3_TFLOPS if x3 else PEAK_FP32_TFLOPS
 
     def attainable(steps, pk):
