@@ -105,11 +105,14 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
 }
 
-template <int BM, int BN, int WM, int WN, bool ADD>
+// OP2: the second A operand -- 0 none, 1 the Res2Net addend (s0.p2, summed into A), 2 the
+// K-concatenated 1x1 operand s1 (projection shortcut / AFF concat: K = taps * s0.cin + s1.cin)
+template <int BM, int BN, int WM, int WN, int OP2>
 __global__ void __launch_bounds__(64 * WM * WN, (FCfg<BM, BN, WM, WN>::WAVES_PER_EU))
 conv_gemm_x3f_kernel(const ConvDesc d) {
   SPK_GATE(d.run_if);
   using C = FCfg<BM, BN, WM, WN>;
+  constexpr bool ADD = OP2 == 1, S1 = OP2 == 2;
   constexpr int TM = C::TM, TN = C::TN, ROWS = C::ROWS, NT = C::NT;
   constexpr int RPP = NT / 8;                          // rows per staging pass
   __shared__ __attribute__((aligned(16))) float lds[C::LDS / 4];
@@ -138,7 +141,9 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
   const __amdgpu_buffer_rsrc_t r0 = make_rsrc(d.s0.p + (size_t)img0 * img_px * d.s0.ld);
   __amdgpu_buffer_rsrc_t r2;
   if (ADD) r2 = make_rsrc(d.s0.p2 + (size_t)img0 * img_px * d.s0.ld2);
-  uint32_t roff[ROWS], roff2[ADD ? ROWS : 1], rmask[ROWS];
+  if (S1) r2 = make_rsrc(d.s1.p + (size_t)img0 * d.s1.H * d.s1.W * d.s1.ld);
+  uint32_t roff[ROWS], roff2[OP2 ? ROWS : 1], rmask[ROWS];
+  uint32_t rvalid = 0;                                // S1: bit r = row r < M
 #pragma unroll
   for (int r = 0; r < ROWS; ++r) {
     const int m = m0 + row0 + RPP * r;
@@ -149,6 +154,9 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
     const int pix = ((img - img0) * d.s0.H + hb) * d.s0.W + wb;   // may be negative: masked
     roff[r] = (uint32_t)pix * (uint32_t)d.s0.ld * 4u;
     if (ADD) roff2[r] = (uint32_t)pix * (uint32_t)d.s0.ld2 * 4u;
+    if (S1)
+      roff2[r] = (uint32_t)((((img - img0) * d.s1.H + ho * d.s1.sh) * d.s1.W + wo * d.s1.sw) * d.s1.ld) * 4u;
+    if (valid) rvalid |= 1u << r;
     const int wl = d.s0.vlen ? min(d.s0.W, d.s0.vlen[img]) : d.s0.W;
     uint32_t mk = 0;
     for (int ky = 0; ky < d.s0.kh; ++ky) {
@@ -163,12 +171,13 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
   }
 
   // ---- scalar K walk: tile start (tap t0, channel c0), pixel deltas of taps t0 and t0 + 1
-  const int cin = d.s0.cin, kw = d.s0.kw;
+  // (past the last tap the walk stays at t0 = taps and c0 counts channels of s1)
+  const int cin = d.s0.cin, kw = d.s0.kw, taps = d.s0.kh * d.s0.kw;
   const int dyW = d.s0.dh * d.s0.W, dx = d.s0.dw;
   int t0, c0, kyB, kxB, tdpA, tdpB;
   {
     const int k = kt0 * FBK;
-    t0 = k / cin;
+    t0 = min(k / cin, taps);
     c0 = k - t0 * cin;
     const int ky = t0 / kw, kx = t0 - ky * kw;
     tdpA = ky * dyW + kx * dx;
@@ -196,28 +205,30 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
 
   struct ASet {
     f32x4 v[ROWS];
-    f32x4 v2[ADD ? ROWS : 1];
+    f32x4 v2[OP2 ? ROWS : 1];
   };
   // issue the A loads of the K-tile at the walk position, then advance the walk by BK
   bool inloop = false;   // (ablation builds)
   auto load_a = [&](ASet& s) {
     const int c = c0 + 4 * kq;
-    const bool sel = c >= cin;                         // this quad lies in tap t0 + 1
+    const bool sel = t0 < taps && c >= cin;            // this quad lies in tap t0 + 1 (or s1)
     const int cc = sel ? c - cin : c;
-    const int t = min(t0 + (sel ? 1 : 0), 31);       // past the last tap (K padding): no mask bit
+    const int t = min(t0 + (sel ? 1 : 0), 31);       // taps: past s0 (s1, or K padding: no mask bit)
     const int tdp = sel ? tdpB : tdpA;
     const uint32_t toff = (uint32_t)(tdp * d.s0.ld + cc) * 4u;
-    const uint32_t toff2 = ADD ? (uint32_t)(tdp * d.s0.ld2 + cc) * 4u : 0u;
+    const uint32_t toff2 = ADD ? (uint32_t)(tdp * d.s0.ld2 + cc) * 4u : (uint32_t)cc * 4u;
+    const bool in1 = S1 && t == taps && cc < d.s1.cin;
 #pragma unroll
     for (int r = 0; r < ROWS; ++r) {
       const bool ok = (rmask[r] >> t) & 1u;
       if (!(SPK_FEXP & 2) || !inloop) {
         s.v[r] = buf_load4(r0, ok ? roff[r] + toff : BUF_OOB);
         if (ADD) s.v2[r] = buf_load4(r2, ok ? roff2[r] + toff2 : BUF_OOB);
+        if (S1) s.v2[r] = buf_load4(r2, (in1 && ((rvalid >> r) & 1u)) ? roff2[r] + toff2 : BUF_OOB);
       }
     }
     c0 += FBK;
-    if (c0 >= cin) {                                   // cin >= 32: one tap boundary per K-tile
+    if (t0 < taps && c0 >= cin) {                      // cin >= 32: one tap boundary per K-tile
       c0 -= cin;
       ++t0;
       tdpA = tdpB;
@@ -232,7 +243,7 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
 #pragma unroll
     for (int r = 0; r < ROWS; ++r) {
       f32x4 v = s.v[r];
-      if (ADD) v += s.v2[r];
+      if (OP2) v += s.v2[r];                           // addend, or s1 (exactly one of the two is nonzero)
       f16x4 h, l;
       split_x3(v, h, l);
       const int off = (row0 + RPP * r) * C::LROW + kq * 4;
@@ -283,7 +294,7 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
     }
   };
 
-  constexpr int ALOADS = ROWS * (ADD ? 2 : 1);       // ordinary loads per A set
+  constexpr int ALOADS = ROWS * (OP2 ? 2 : 1);       // ordinary loads per A set
   // Pairs of K-tiles (even step: LDS buffer 0, odd step: buffer 1; A register sets 0 / 1 two
   // K-tiles ahead), an odd last K-tile peeled after the loop: the loop has one back edge, so
   // hipcc's wait counting sees the same loads in flight on both paths into its header (with a
@@ -412,6 +423,10 @@ struct FTile {
   int bm, bn;
 };
 
+// the two-operand forms (the naming probe of runtime.cpp sets the sizes without pointers)
+bool has_add(const ConvDesc& d) { return d.s0.p2 != nullptr || d.s0.ld2 > 0; }
+bool has_s1(const ConvDesc& d) { return d.s1.p != nullptr || d.s1.cin > 0; }
+
 // tile per layer: SPK_GEMM_F_TILE=128x128 | 256x128 | 128x256 | 256x256 overrides (experiments)
 FTile f_tile(const ConvDesc& d) {
   static const int forced = [] {
@@ -424,7 +439,7 @@ FTile f_tile(const ConvDesc& d) {
     case 1: return {128, 128};
     case 2: return {256, 128};
     case 3: return {128, 256};
-    case 4: return d.s0.p2 ? FTile{128, 128} : FTile{256, 256};
+    case 4: return (has_add(d) || has_s1(d)) ? FTile{128, 128} : FTile{256, 256};
     default: break;
   }
   // measured (tools/gemm_bench, ERes2NetV2 B = 256 layer shapes, round 5): the 256 x 256 tile
@@ -434,10 +449,11 @@ FTile f_tile(const ConvDesc& d) {
   // 2067 -> 1766); the 104-wide layers keep 128 x 128 at two blocks per CU
   // Two conditions keep a layer off it: a last round of blocks that leaves most CUs idle (one
   // block per CU: ECAPA's 1x1 convs at B = 256, 792 blocks = 3.1 rounds, 0.39 -> 0.55 ms), and
-  // a short K with an epilogue that reads operands (fuse34's AFF conv, K = 256: its epilogue
-  // is not overlapped by a second resident block, 0.22 -> 0.25 ms).
+  // a short K with the AFF epilogue (fuse34's local_att.3, K = 256: its epilogue reads two
+  // operands and is not overlapped by a second resident block, 0.22 -> 0.25 ms; the residual
+  // conv3s of layer 3, K = 208, gain: 425 -> 396 us).
   const int M = d.nimg * d.Ho * d.Wo;
-  if (d.N > 128 && M >= 16384 && !d.s0.p2 && (d.Kp >= 512 || (!d.res && !d.affx && !d.gate))) {
+  if (d.N > 128 && M >= 16384 && !has_add(d) && !has_s1(d) && (d.Kp >= 512 || (!d.affx && !d.gate))) {
     static int cus = 0;
     if (!cus) {
       int dev = 0, n = 0;
@@ -456,11 +472,14 @@ hipError_t launch_f_t(const ConvDesc& d, hipStream_t s) {
   const int M = d.nimg * d.Ho * d.Wo;
   const int nblk = ((M + BM - 1) / BM) * ((d.N + BN - 1) / BN);
   dim3 grid(nblk, 1, d.ksplit);
-  if (d.s0.p2) {
-    if constexpr (BM * BN >= 256 * 256) return hipErrorInvalidValue;   // f_tile: 128 x 128 for the addend form
-    else hipLaunchKernelGGL((conv_gemm_x3f_kernel<BM, BN, WM, WN, true>), grid, dim3(64 * WM * WN), 0, s, d);
+  const dim3 blk(64 * WM * WN);
+  if (d.s0.p2 || d.s1.p) {
+    // f_tile: 128 x 128 for the two-operand forms (the 256 x 256 one spills)
+    if constexpr (BM * BN >= 256 * 256) return hipErrorInvalidValue;
+    else if (d.s0.p2) hipLaunchKernelGGL((conv_gemm_x3f_kernel<BM, BN, WM, WN, 1>), grid, blk, 0, s, d);
+    else hipLaunchKernelGGL((conv_gemm_x3f_kernel<BM, BN, WM, WN, 2>), grid, blk, 0, s, d);
   } else {
-    hipLaunchKernelGGL((conv_gemm_x3f_kernel<BM, BN, WM, WN, false>), grid, dim3(64 * WM * WN), 0, s, d);
+    hipLaunchKernelGGL((conv_gemm_x3f_kernel<BM, BN, WM, WN, 0>), grid, blk, 0, s, d);
   }
   return hipGetLastError();
 }
@@ -475,16 +494,18 @@ bool gemm_f_supported(const ConvDesc& d) {
   const int M = d.nimg * d.Ho * d.Wo;
   const FTile t = f_tile(d);
   return !off && d.wf && d.wh && d.wl && !d.wbig && !d.x1 && !d.kcb && !d.s0.reflect && !d.s0.pre_scale &&
-         !d.s1.p && d.s1.cin == 0 && d.N > 64 && M > 4096 && d.Kp % FBK == 0 && d.Kp >= d.K &&
+         d.N > 64 && M > 4096 && d.Kp % FBK == 0 && d.Kp >= d.K && !(has_add(d) && has_s1(d)) &&
+         // K-concatenated s1: a 1x1 operand with the output's geometry (strided rows allowed)
+         (!has_s1(d) || (d.s1.cin % 4 == 0 && d.s1.ld % 4 == 0 && d.K == d.s0.kh * d.s0.kw * d.s0.cin + d.s1.cin)) &&
          conv_buf_loader_ok(d, t.bm);
 }
 
 std::string gemm_f_kernel_name(const ConvDesc& d) {
-  const bool add = d.s0.p2 != nullptr || d.s0.ld2 > 0;
+  const bool add = d.s0.p2 != nullptr || d.s0.ld2 > 0, s1 = d.s1.p != nullptr || d.s1.cin > 0;
   const FTile t = f_tile(d);
   const int wm = t.bm == 256 && t.bn == 128 ? 4 : 2, wn = 8 / wm;
   return "conv_gemm_x3f_kernel<" + std::to_string(t.bm) + ", " + std::to_string(t.bn) + ", " + std::to_string(wm) +
-         ", " + std::to_string(wn) + ", " + (add ? "true" : "false") + ">";
+         ", " + std::to_string(wn) + ", " + (add ? "1" : s1 ? "2" : "0") + ">";
 }
 
 hipError_t launch_gemm_f(const ConvDesc& d, hipStream_t s) {

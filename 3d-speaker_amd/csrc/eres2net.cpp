@@ -202,13 +202,14 @@ struct ERes2Builder {
     return bout;
   }
 
-  // The whole block as one fused kernel (res2block.hip / res2block_s2.hip), scale 2, fp16x3
-  // path, uniform lengths: stage 1 (slices <= 32 wide, 128 output channels) -- identity
-  // shortcut from 128 channels, or the stage's first block with a 1x1 stride-1 projection
-  // shortcut from 64; stage 2 (slices 33..64, 256 output channels) -- identity from 256, or
-  // the first block: 1x1 stride-2 conv1 and projection shortcut from 128.
+  // The whole block as one fused kernel (res2block.hip), scale 2, fp16x3 path, uniform
+  // lengths: stage 1 (slices <= 32 wide, 128 output channels) -- identity shortcut from 128
+  // channels, or the stage's first block with a 1x1 stride-1 projection shortcut from 64.
   // (ERes2Net's BasicBlockERes2Net, ERes2Net.py:61-87, has the forward of ERes2NetV2's block,
-  // ERes2NetV2.py:65-91: ERes2Net-large's stage 1 -- width 32 -- takes the same kernel)
+  // ERes2NetV2.py:65-91: ERes2Net-large's stage 1 -- width 32 -- takes the same kernel.)
+  // Stage 2 runs as four kernels (1x1 GEMM, two halo 3x3 convs, 1x1 + residual): a fused
+  // stage-2 kernel (rounds 3-4) measured slower than those after the round-4 epilogue work
+  // (ERes2NetV2 layer2 6.77 vs 5.91 ms) and was removed in round 5.
   bool fusable(const std::string& p, const T4& x, int stride, int width, int Cout, bool use_aff) const {
     const bool sc = m.has(p + ".shortcut.0.weight");
     const bool common = !use_aff && scale == 2 && x.ld == x.C && !b.ragged && b.x3() &&
@@ -216,26 +217,13 @@ struct ERes2Builder {
     // stage 1 (res2block.hip): slices <= 32, 128 output channels, identity or 64 -> 128 projection
     const bool s1 = stride == 1 && width <= 32 && Cout == 128 &&
                     (sc ? (x.C == 64 && std::getenv("SPK_NO_PROJ_FUSION") == nullptr) : x.C == 128);
-    // stage 2 (res2block_s2.hip): slices 33..64, 256 -> 256 identity, or 128 -> 256 at stride 2
-    // with the projection shortcut
-    // Stage 2 runs unfused unless SPK_S2_FUSION=1: since the round-4 epilogue work the four
-    // kernels of a block (1x1 GEMM, two halo 3x3 convs, 1x1 + residual) beat the fused kernel
-    // on MI355X -- ERes2NetV2 layer2 5.91 vs 6.77 ms, forward 24.05 vs 25.27 ms (two reps each);
-    // ERes2Net-large 1.55 vs 1.70 ms per block
-    static const bool s2_on = [] {
-      const char* e = std::getenv("SPK_S2_FUSION");
-      return e && std::string(e) == "1";
-    }();
-    const bool s2 = s2_on && width > 32 && width <= 64 && Cout == 256 &&
-                    (sc ? (x.C == 128 && stride == 2 && std::getenv("SPK_NO_PROJ_FUSION") == nullptr)
-                        : (x.C == 256 && stride == 1));
-    return common && (s1 || s2);
+    return common && s1;
   }
 
   bool fused_block(const std::string& p, const T4& x, int stride, int width, int Cout, Buf outbuf, T4& out) {
     const ChanMap xin = ChanMap::dense(x.C);
     const ChanMap om = ChanMap::dense(Cout);
-    const int sw = width <= 32 ? 32 : 64;   // padded slice width of the fused kernel
+    const int sw = 32;                      // padded slice width of the fused kernel
     const ChanMap sl = ChanMap::slices(width, 2, sw);
     const ChanMap wsw = ChanMap::dense(width, sw);
     const bool proj = m.has(p + ".shortcut.0.weight");
@@ -245,8 +233,6 @@ struct ERes2Builder {
     std::vector<Part> parts3{Part{p + ".conv3.weight", "", p + ".bn3", sl, 0, 0}};
     if (proj) parts3.push_back(Part{p + ".shortcut.0.weight", "", p + ".shortcut.1", xin, 0, 2 * sw});
     const Packed& c3 = m.pack(p + ".conv3#fused", om, parts3, 2 * sw + (proj ? x.C : 0));
-    // the stage-2 kernel's 3x3 convs use the one-accumulator fp16x3 form (hi_w scaled by 2^11)
-    if (sw == 64 && (ca.wmax >= kX3WeightLimit || cb.wmax >= kX3WeightLimit)) return false;
     const int Ho = (x.H - 1) / stride + 1, Wo = (x.W - 1) / stride + 1;
     const double px = (double)Ho * Wo;   // output pixels (a strided block reads only those inputs)
     b.macs_per_utt += px * x.C * (double)width * 2 + 2.0 * px * 9.0 * width * width + px * (double)width * 2 * Cout +

@@ -31,10 +31,6 @@ struct Res2Desc {
 };
 
 bool res2_block_supported(const Res2Desc& d);
-// stage-2 blocks (slices 33..64 wide): the 256 -> 256 identity blocks and the stage's first
-// block (128 -> 256, stride 2, 1x1 projection shortcut): res2block_s2.hip
-bool res2_block_s2_supported(const Res2Desc& d);
-hipError_t launch_res2_block_s2(const Res2Desc& d, hipStream_t s);
 hipError_t launch_res2_block(const Res2Desc& d, hipStream_t s);
 std::string res2_block_kernel_name(const Res2Desc& d);
 

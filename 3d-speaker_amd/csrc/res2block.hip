@@ -497,7 +497,6 @@ int device_cus_r2() {
 }  // namespace
 
 bool res2_block_supported(const Res2Desc& d) {
-  if (res2_block_s2_supported(d)) return true;
   const int co = d.Cout ? d.Cout : d.C;
   const bool shape = d.stride == 1 && (!d.Hin || d.Hin == d.H) && (!d.Win || d.Win == d.W) &&
                      (d.proj ? (d.C == 64 && co == 128) : (d.C == 128 && co == 128));
@@ -506,12 +505,10 @@ bool res2_block_supported(const Res2Desc& d) {
 }
 
 std::string res2_block_kernel_name(const Res2Desc& d) {
-  if (res2_block_s2_supported(d)) return d.proj ? "res2_block_s2_kernel<true>" : "res2_block_s2_kernel<false>";
   return d.proj ? "res2_block_kernel<64, 128, true>" : "res2_block_kernel<128, 128, false>";
 }
 
 hipError_t launch_res2_block(const Res2Desc& d, hipStream_t s) {
-  if (res2_block_s2_supported(d)) return launch_res2_block_s2(d, s);
   if (!res2_block_supported(d) || d.x == d.out) return hipErrorInvalidValue;
   const int ntiles = d.nimg * ((d.W + 15) / 16) * ((d.H + 7) / 8);
   int grid = std::min(device_cus_r2(), (ntiles + 7) / 8 * 8);

@@ -234,7 +234,7 @@ bool conv_use_x3() {
   return !(e && std::string(e) == "f32");
 }
 
-// fused Res2Net block (res2block.hip, res2block_s2.hip), the kernels' contract in double
+// fused Res2Net block (res2block.hip), the kernels' contract in double
 // precision: conv1 + bn1 + Hardtanh -> s0 | s1 (slices padded to SW = 32 or 64 channels),
 // y0 = Ht(conv3x3(s0)), y1 = Ht(conv3x3(y0 + s1)), out = Ht(conv3(cat(y0, y1)) + x) -- or,
 // with the projection shortcut, Ht(conv3(cat(y0, y1, x))) -- zero padding at the edges; conv1

@@ -91,8 +91,8 @@ def test_step_bytes_priced_per_conv():
     names = [name for name, _, _ in steps]
     px3 = B * 20 * (T // 4)
     assert nbytes[names.index("layer3.1.conv3")] == 4.0 * (px3 * 208 + 512 * 208 + px3 * 512 + px3 * 512)
-    # the stage-2 blocks run unfused by default (four kernels measured faster than
-    # res2block_s2.hip): conv3 (1x1, 104 -> 256, residual) priced like layer3's
+    # the stage-2 blocks run unfused (four kernels measured faster than a fused stage-2 kernel,
+    # DESIGN.md §7 round 4): conv3 (1x1, 104 -> 256, residual) priced like layer3's
     px2 = B * 40 * (T // 2)
     assert 'layer2.1.fused' not in names
     assert nbytes[names.index('layer2.1.conv3')] == 4.0 * (px2 * 104 + 256 * 104 + px2 * 256 + px2 * 256)

@@ -37,6 +37,7 @@ struct Shape {
   int nimg, H, W, cin, N, k, s, act;
   bool res;
   int addend;   // Res2Net addend operand (s0.p2)
+  int s1cin = 0, s1H = 0, s1W = 0, s1s = 1;   // K-concatenated 1x1 operand (projection shortcut)
 };
 
 // ERes2NetV2 (m_channels 64, baseWidth 26, scale 2, expansion 2) at B = 256, T = 198
@@ -50,6 +51,9 @@ static const Shape kShapes[] = {
     {"l4.convs0", 256, 10, 25, 208, 208, 3, 1, ACT_HTANH, false, 0},
     {"l3_ds", 256, 20, 50, 512, 1024, 3, 2, ACT_NONE, false, 0},
     {"l2.conv1", 256, 40, 99, 256, 104, 1, 1, ACT_HTANH, false, 0},
+    {"l2.0.conv3", 256, 40, 99, 104, 256, 1, 1, ACT_HTANH, false, 0, 128, 80, 198, 2},
+    {"l3.0.conv3", 256, 20, 50, 208, 512, 1, 1, ACT_HTANH, false, 0, 256, 40, 99, 2},
+    {"fuse34.att0", 256, 10, 25, 1024, 256, 1, 1, ACT_SILU, false, 0, 1024, 10, 25, 1},
 };
 
 struct Lib {
@@ -89,18 +93,25 @@ int main(int argc, char** argv) {
     const int pad = sh.k / 2;
     const int Ho = (sh.H + 2 * pad - sh.k) / sh.s + 1, Wo = (sh.W + 2 * pad - sh.k) / sh.s + 1;
     const int M = sh.nimg * Ho * Wo;
-    const int taps = sh.k * sh.k, K = taps * sh.cin, Kp = round_up(K, 32);
+    const int taps = sh.k * sh.k, K0 = taps * sh.cin, K = K0 + sh.s1cin, Kp = round_up(K, 32);
     const size_t nin = (size_t)sh.nimg * sh.H * sh.W * sh.cin;
+    const size_t nin1 = (size_t)sh.nimg * sh.s1H * sh.s1W * sh.s1cin;
     std::vector<float> x(nin), x2(sh.addend ? nin : 0), w((size_t)sh.N * Kp, 0.f), b(sh.N), r(sh.res ? (size_t)M * sh.N : 0);
     std::uniform_real_distribution<float> ua(0.f, 2.f), uw(-1.f, 1.f);
     for (auto& v : x) v = ua(rng);
     for (auto& v : x2) v = ua(rng);
+    std::vector<float> x1(nin1);
+    for (auto& v : x1) v = ua(rng);
     const float ws = 1.0f / std::sqrt((float)K);
     for (int n = 0; n < sh.N; ++n)
       for (int k = 0; k < K; ++k) w[(size_t)n * Kp + k] = uw(rng) * ws;
     for (auto& v : b) v = uw(rng) * 0.1f;
     for (auto& v : r) v = ua(rng);
-    float *dx, *dx2 = nullptr, *dw, *db, *dr = nullptr, *dout;
+    float *dx, *dx2 = nullptr, *dx1 = nullptr, *dw, *db, *dr = nullptr, *dout;
+    if (nin1) {
+      CK(hipMalloc(&dx1, nin1 * 4));
+      CK(hipMemcpy(dx1, x1.data(), nin1 * 4, hipMemcpyHostToDevice));
+    }
     uint16_t *dwh, *dwl;
     CK(hipMalloc(&dx, nin * 4));
     if (sh.addend) CK(hipMalloc(&dx2, nin * 4));
@@ -123,6 +134,10 @@ int main(int argc, char** argv) {
     d.nimg = sh.nimg; d.Ho = Ho; d.Wo = Wo; d.N = sh.N; d.K = K; d.Kp = Kp;
     d.w = dw; d.wh = dwh; d.wl = dwl; d.bias = db; d.out = dout; d.ldo = sh.N; d.act = sh.act;
     d.res = dr; d.ldr = sh.res ? sh.N : 0;
+    if (nin1) {
+      d.s1.p = dx1; d.s1.ld = sh.s1cin; d.s1.cin = sh.s1cin; d.s1.H = sh.s1H; d.s1.W = sh.s1W;
+      d.s1.sh = d.s1.sw = sh.s1s;
+    }
 
     // host reference of sampled outputs (fp64)
     std::vector<int> sm, sn;
@@ -146,13 +161,26 @@ int main(int argc, char** argv) {
             a += std::fabs(p);
           }
         }
+      if (nin1) {
+        const size_t px1 = ((size_t)img * sh.s1H + ho * sh.s1s) * sh.s1W + wo * sh.s1s;
+        for (int c = 0; c < sh.s1cin; ++c) {
+          const double p = (double)x1[px1 * sh.s1cin + c] * w[(size_t)n * Kp + K0 + c];
+          acc += p;
+          a += std::fabs(p);
+        }
+      }
       if (sh.res) { acc += r[(size_t)m * sh.N + n]; a += std::fabs(r[(size_t)m * sh.N + n]); }
       if (sh.act == ACT_HTANH) acc = std::min(std::max(acc, 0.0), 20.0);
+      if (sh.act == ACT_SILU) {
+        const double a0 = a;
+        acc = acc / (1.0 + std::exp(-acc));
+        a = a0;
+      }
       ref[i] = acc;
       mag[i] = a;
     }
     const double flop = 2.0 * M * (double)K * sh.N;
-    const double bytes = 4.0 * ((double)nin * (sh.addend ? 2 : 1) + (double)M * sh.N * (sh.res ? 2 : 1));
+    const double bytes = 4.0 * ((double)nin * (sh.addend ? 2 : 1) + (double)M * sh.s1cin + (double)M * sh.N * (sh.res ? 2 : 1));
     std::printf("%-10s M=%d K=%d N=%d  %.1f GFLOP  %.0f MB\n", sh.name, M, K, sh.N, flop * 1e-9, bytes * 1e-6);
     for (const Lib& L : libs) {
       CK(L.split(dw, dwh, dwl, w.size(), st));
@@ -191,7 +219,7 @@ int main(int argc, char** argv) {
       std::fflush(stdout);
       if (dwf) CK(hipFree(dwf));
     }
-    CK(hipFree(dx)); if (dx2) CK(hipFree(dx2)); CK(hipFree(dw)); CK(hipFree(dwh)); CK(hipFree(dwl)); CK(hipFree(db));
+    CK(hipFree(dx)); if (dx2) CK(hipFree(dx2)); if (dx1) CK(hipFree(dx1)); CK(hipFree(dw)); CK(hipFree(dwh)); CK(hipFree(dwl)); CK(hipFree(db));
     if (dr) CK(hipFree(dr)); CK(hipFree(dout));
   }
   return 0;
