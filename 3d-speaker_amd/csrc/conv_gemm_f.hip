@@ -32,6 +32,13 @@
 #include "conv_epilogue.h"
 #include "conv_loader.h"
 
+#ifndef SPK_F_SCHED
+#define SPK_F_SCHED 5   // loop schedule: 1 the one-set (256 x 256) loop splits + stores the next A
+                        // set between its two k-steps (measured -5..-17 % on the N > 128 layers;
+                        // 0: after both), 2 static priority for the second half of the waves
+                        // (mixed, off), 4 the two-set loop splits between its k-steps too (0-3 %
+                        // on the 128 x 128 layers)
+#endif
 #ifndef SPK_FEXP
 #define SPK_FEXP 0   // ablation builds only (tools/fexp.sh), bit mask: 1 no MFMA, 2 no in-loop A loads,
                      // 4 no in-loop A split / stores, 8 no in-loop B DMA, 16 no epilogue stores
@@ -261,11 +268,11 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int li = lane & 31, lh = lane >> 5;
-  auto compute = [&](int buf) {
+  // one 16-deep k-step of a K-tile (s = 0, 1)
+  auto compute_s = [&](int buf, int s) {
     const _Float16* ahi = reinterpret_cast<const _Float16*>(lb + buf * C::STAGE);
     const char* bb = lb + buf * C::STAGE + C::ASTAGE + wn * TN * 4096 + lane * 16;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    {
       f16x8 ah[TM], al[TM], bh[TN], bl[TN], bh2[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -293,6 +300,10 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
         }
     }
   };
+  auto compute = [&](int buf) {
+    compute_s(buf, 0);
+    compute_s(buf, 1);
+  };
 
   constexpr int ALOADS = ROWS * (OP2 ? 2 : 1);       // ordinary loads per A set
   // Pairs of K-tiles (even step: LDS buffer 0, odd step: buffer 1; A register sets 0 / 1 two
@@ -313,18 +324,34 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALOADS) : "memory");   // B of kt0 landed
     __syncthreads();
     inloop = true;
+#if SPK_F_SCHED & 2
+    if (wave >= C::NT / 128) __builtin_amdgcn_s_setprio(1);   // the second-dispatched half of the waves
+#endif
     for (int kt = kt0; kt < kt1; ++kt) {
       const int buf = (kt - kt0) & 1;
       dma_b(min(kt + 1, kt1 - 1), buf ^ 1);           // buffer buf ^ 1 was read before the last barrier
+#if SPK_F_SCHED & 1
+      // the A set's split + LDS stores between the two k-steps: its VALU / LDS work issues in
+      // the gaps of the second k-step's MFMAs
+      compute_s(buf, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      store_a(buf ^ 1, set);
+      load_a(set);
+      compute_s(buf, 1);
+#else
       compute(buf);
       // keep the split of the A set (loaded at the end of the previous step) behind the MFMAs:
       // hoisted to the top of the step it waited for those loads before any MFMA could issue
       __builtin_amdgcn_sched_barrier(0);
       store_a(buf ^ 1, set);                           // K-tile kt + 1 (past the end: unused)
       load_a(set);                                     // kt + 2
+#endif
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALOADS) : "memory");   // B of kt + 1 landed
       __syncthreads();
     }
+#if SPK_F_SCHED & 2
+    __builtin_amdgcn_s_setprio(0);
+#endif
   } else if (kt0 < kt1) {
     ASet set0, set1;
     dma_b(kt0, 0);
@@ -339,17 +366,31 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
       // even step: buffer 0 holds kt; set 1 holds kt + 1 (in flight)
       dma_b(kt + 1, 1);
       load_a(set0);                                    // kt + 2
+#if SPK_F_SCHED & 4
+      compute_s(0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      store_a(1, set1);
+      compute_s(0, 1);
+#else
       compute(0);
       __builtin_amdgcn_sched_barrier(0);
       store_a(1, set1);
+#endif
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALOADS) : "memory");   // B of kt + 1 landed
       __syncthreads();
       // odd step: buffer 1 holds kt + 1; set 0 holds kt + 2 (in flight)
       dma_b(min(kt + 2, kt1 - 1), 0);
       load_a(set1);                                    // kt + 3
+#if SPK_F_SCHED & 4
+      compute_s(1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      store_a(0, set0);
+      compute_s(1, 1);
+#else
       compute(1);
       __builtin_amdgcn_sched_barrier(0);
       store_a(0, set0);
+#endif
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALOADS) : "memory");
       __syncthreads();
     }

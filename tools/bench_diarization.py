@@ -100,6 +100,14 @@ def main():
         np.random.seed(0)
         lk = cc(emb, speaker_num=args.speakers)
         res['spectral_k_der'] = der_of(vad_post.compressed_seg([[c[0], c[1], int(j)] for c, j in zip(chunks, lk)]))
+        # ... and without the centroid merge (mer_cos): with the synthetic weights every
+        # embedding pair sits at cosine 0.87-0.99, so merging centroids above 0.8 folds the four
+        # true speakers into one; the partition itself separates them
+        # (tests/test_gpu_c5_full.py checks it against the oracle pipeline)
+        np.random.seed(0)
+        lk2 = cluster.spectral_labels_gpu(emb, oracle_num=args.speakers)
+        res['spectral_k_nomerge_speakers'] = int(len(np.unique(lk2)))
+        res['spectral_k_nomerge_der'] = der_of(vad_post.compressed_seg([[c[0], c[1], int(j)] for c, j in zip(chunks, lk2)]))
     total = sum(v for k, v in t.items() if k != 'synth_s')
     res.update({k: round(v, 3) for k, v in t.items()})
     res['pipeline_s'] = round(total, 3)
