@@ -79,25 +79,52 @@ struct ConvDesc {
   // the weights in MFMA fragment order for the LDS-DMA GEMM (conv_gemm_f.hip launch_pack_frag;
   // null: that kernel is not used)
   const uint16_t* wf = nullptr;
+  const int* range_in = nullptr;  // scaled split (below): the forward's range word, read for the operand scale
 };
 
 // fp16x3 range guard.  The split-precision GEMMs represent an operand as two fp16 values,
 // so an activation at or above fp16's largest finite value (65504) would saturate silently.
 // Every producer of an unbounded activation that a split GEMM later reads (conv / linear
-// epilogues, the ERes2Net stem, AFF, the model input) ORs 1 into the forward's range word
-// (a slot of the caller's workspace, zeroed at the start of every forward) when any output
-// it writes reaches kRangeLimit.  The ops between two GEMMs grow a value at most 2x (AFF
-// combine: |x t + y (2 - t)| <= 2 max(|x|, |y|); residual + Hardtanh), so every operand a
-// split GEMM reads stays below 2 kRangeLimit = 2^15 < 65504 (a limit of 2^15 would let a
-// doubled 32767.9 reach 65535.8, past fp16's largest finite value).  The exact-fp32 plan is
-// captured behind the fp16x3 one on the same stream with its launches gated on that word
-// (launch_gate), so a flagged batch is recomputed on the device, without a host round trip.
+// epilogues, the ERes2Net stem, AFF, the model input) raises the forward's range word (a slot
+// of the caller's workspace, zeroed at the start of every forward) to the bit pattern of the
+// largest |output| it writes, when that reaches kRangeLimit (atomicMax on the bits of a
+// non-negative float orders like the floats; the word stays 0 while everything is in range).
+// The ops between two GEMMs grow a value at most 2x (AFF combine: |x t + y (2 - t)| <=
+// 2 max(|x|, |y|); residual + Hardtanh; the Res2Net addend), so while the word is 0 every
+// operand a split GEMM reads stays below 2 kRangeLimit = 2^15 < 65504 (a limit of 2^15 would
+// let a doubled 32767.9 reach 65535.8, past fp16's largest finite value).  A set word is
+// resolved one of two ways, both on the device without a host round trip:
+//  - exact twin (ERes2Net*, ResNet): the exact-fp32 plan is captured behind the fp16x3 one on
+//    the same stream with its launches gated on the word (launch_gate);
+//  - scaled split (ECAPA, CAM++: every split GEMM of the plan takes ConvDesc::range_in): a
+//    GEMM multiplies the operand it splits by range_scale(word) = 2^-s, s chosen so that
+//    word * 2^-s < kRangeLimit, and its accumulator by 2^s (both exact: powers of two).  Every
+//    operand is at most twice the largest value any earlier producer wrote, which the word
+//    holds by the time the GEMM starts, so the scaled operand stays below 2^15; relative
+//    precision is that of the unscaled split.  A block may read a larger word than another
+//    (producers of its own launch raising it meanwhile): each block undoes its own scale, so
+//    every output is consistent.
 constexpr float kRangeLimit = 16384.0f;
 // the tiled fp16x3 GEMM scales the weights' hi plane by 2^11 (conv_gemm.hip): 31.5 * 2^11 < 65504
 constexpr float kX3WeightLimit = 31.5f;
 #ifdef __HIPCC__
 __device__ __forceinline__ void range_note(int* flag, float amax) {
-  if (flag && amax >= kRangeLimit) atomicOr(flag, 1);
+  if (flag && amax >= kRangeLimit) atomicMax(flag, __float_as_int(amax));
+}
+// operand scale of a scaled-split GEMM (above): 1 while the word is clear (or absent, or
+// non-finite: the result is inf / NaN either way), else 2^-s with word * 2^-s in [2^13, 2^14)
+__device__ __forceinline__ float range_scale(const int* word) {
+  if (!word) return 1.f;
+  const int w = *word;
+  if (w < 0x46800000 || w >= 0x7F800000) return 1.f;       // below 2^14 (i.e. 0), or inf / NaN
+  const int e = (w >> 23) - 127;                             // word in [2^e, 2^(e+1)), e >= 14
+  return __int_as_float((127 - (e - 13)) << 23);             // 2^-(e-13)
+}
+// 2^k * sc and 2^k / sc of a power-of-two scale by exponent arithmetic (scalar integer ops:
+// the values stay in SGPRs instead of taking a VGPR each for a float multiply / divide)
+__device__ __forceinline__ float pow2_mul(float sc, int k) { return __int_as_float(__float_as_int(sc) + k * (1 << 23)); }
+__device__ __forceinline__ float pow2_div(float sc, int k) {
+  return __int_as_float(0x7F000000 + k * (1 << 23) - __float_as_int(sc));
 }
 // Time reductions with one lane per channel (TDNN statistics, TSTP pooling) are latency-
 // bound: a frame's load feeds a serial update, so a wave keeps only a load or two in flight.

@@ -342,6 +342,8 @@ __global__ void __launch_bounds__(64 * (PIX / 32) * KS, 1)
 conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
   SPK_GATE(d.run_if);
   using C = HaloX3Cfg<CIN, PIX, KS, SH>;
+  // scaled split (common.h): operand x 2^-s at staging, accumulators x 2^s after the taps
+  const float sc = range_scale(d.range_in), back = pow2_div(sc, 0), back_x = pow2_div(sc, -11);
   typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
   typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) float lds[C::LDS];
@@ -414,19 +416,21 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
   };
   auto pf_store = [&](auto setc) {
     constexpr int S = decltype(setc)::value;
+    split_pass(sc, [&](auto split) {                // scaled split (common.h) when the word is set
 #pragma unroll
-    for (int r = 0; r < C::PF; ++r) {
-      const int idx = tid + C::NT * r;
-      if (idx < hq) {
-        f32x4 v = pa[S][r];
-        if (ADD) v += pb[S][r];
-        const int q = qq, p = idx / C::QP;
-        f16x4 h, l;
-        split_x3(v, h, l);
-        *reinterpret_cast<f16x4*>(hh + p * C::ROW + 4 * q) = h;
-        *reinterpret_cast<f16x4*>(hlo + p * C::ROW + 4 * q) = l;
+      for (int r = 0; r < C::PF; ++r) {
+        const int idx = tid + C::NT * r;
+        if (idx < hq) {
+          f32x4 v = pa[S][r];
+          if (ADD) v += pb[S][r];
+          const int q = qq, p = idx / C::QP;
+          f16x4 h, l;
+          split(v, h, l);
+          *reinterpret_cast<f16x4*>(hh + p * C::ROW + 4 * q) = h;
+          *reinterpret_cast<f16x4*>(hlo + p * C::ROW + 4 * q) = l;
+        }
       }
-    }
+    });
   };
   using Set0 = std::integral_constant<int, 0>;
   using Set1 = std::integral_constant<int, NSET - 1>;
@@ -494,7 +498,7 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
         accx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, accx, 0, 0, 0);
       }
     }
-    acc[0][0] += accx * (1.0f / 2048.0f);
+    acc[0][0] = acc[0][0] * back + accx * back_x;
     __syncthreads();                                // halo reads done: the epilogue reuses it
     const int img = t / (ntx * nty), ty = (t / ntx) % nty, tx = t % ntx;
     const int y0 = ty * TH, x0 = tx * TW;

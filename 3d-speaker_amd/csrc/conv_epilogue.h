@@ -67,6 +67,46 @@ __device__ __forceinline__ void split_x3(const f32x4 v, h16x4& h, h16x4& l) {
 #endif
 }
 
+// split of sc * v (scaled split, common.h: sc = 2^-s, an SGPR) with the scale folded into
+// the conversions, so the scaled quad is never materialised (a separate multiply measured
+// +3 VGPRs and spills on the 128x128 tiled GEMM): hi = fp16(sc v) by v_fma_mix{lo,hi} (the
+// product exact, one round to nearest), lo = fp16(2^11 sc v - 2^11 hi) as in split_lo2
+__device__ __forceinline__ uint32_t split_hi2s(float v0, float v1, float sc) {
+  uint32_t r;
+  asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
+      "v_fma_mixhi_f16 %0, %3, %2, 0"
+      : "=&v"(r)
+      : "v"(v0), "v"(sc), "v"(v1));
+  return r;
+}
+__device__ __forceinline__ uint32_t split_lo2s(uint32_t hp, float a0, float a1) {   // a = 2^11 sc v
+  uint32_t r;
+  const float m = -2048.0f;
+  asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %1, %2, %4 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(r)
+      : "v"(hp), "s"(m), "v"(a0), "v"(a1));
+  return r;
+}
+__device__ __forceinline__ void split_x3s(const f32x4 v, float sc, h16x4& h, h16x4& l) {
+  typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+  const float c = pow2_mul(sc, 11);
+  const uint32_t h01 = split_hi2s(v[0], v[1], sc);
+  const uint32_t h23 = split_hi2s(v[2], v[3], sc);
+  h = __builtin_bit_cast(h16x4, u32x2v{h01, h23});
+  l = __builtin_bit_cast(h16x4, u32x2v{split_lo2s(h01, v[0] * c, v[1] * c), split_lo2s(h23, v[2] * c, v[3] * c)});
+}
+
+// One staging pass of A operands: `f(split)` stores the pass's rows through `split(v, h, l)`,
+// instantiated twice behind one uniform branch -- the plain split while the range word is clear
+// (sc == 1: the VALU count of the unscaled kernels; the folded scaled split costs one more VALU
+// per value pair, measured +25 % on the VALU-bound 128x128 tiles), the scaled one otherwise.
+template <class F>
+__device__ __forceinline__ void split_pass(float sc, F&& f) {
+  if (sc == 1.0f) f([](const f32x4& v, h16x4& h, h16x4& l) { split_x3(v, h, l); });
+  else f([sc](const f32x4& v, h16x4& h, h16x4& l) { split_x3s(v, sc, h, l); });
+}
+
 // Output store of the fused blocks' conv3 (res2block*.hip).  SPK_NT_STORE=1 (experiment
 // builds): non-temporal, so the block's output does not displace its input halo from L2.
 #ifndef SPK_NT_STORE

@@ -200,13 +200,11 @@ struct X3Cfg {
 // X1 = the single-product variant (C3's reduced-precision mode, spk_model_config_t
 // precision = SPK_PRECISION_FP16): operands rounded to fp16 (round to nearest), one MFMA
 // per product, fp32 accumulation; only the hi planes are staged.
-template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE, bool BUF, bool X1>
-__device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
-  SPK_GATE(d.run_if);
+template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE, bool BUF, bool X1, bool SC>
+__device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d, float* lds, float sc_arg) {
   using C = X3Cfg<BM, BN, WM, WN, X1>;
   constexpr int BK = C::BK, TM = C::TM, TN = C::TN, RPP = C::RPP, AROWS = C::AROWS;
   static_assert(TM >= 1 && TN >= 1 && BM % RPP == 0, "tile shape");
-  __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
   _Float16* hl = reinterpret_cast<_Float16*>(lds);
 
   const int tid = threadIdx.x;
@@ -219,6 +217,13 @@ __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
   const int mt = lid / nN, nt = lid % nN;
   const int m0 = mt * BM, n0 = nt * BN;
 
+  // scaled split (common.h): operand x 2^-s at staging, accumulator x 2^s before the epilogue
+  // (SC = false: the in-range instance, scale 1 at compile time)
+  const float sc = SC ? sc_arg : 1.0f;
+  const auto split = [sc](const f32x4& v, h16x4& h, h16x4& l) {
+    if constexpr (SC) split_x3s(v, sc, h, l);
+    else split_x3(v, h, l);
+  };
   const int nkt_all = d.Kp / BK;
   const int per = (nkt_all + d.ksplit - 1) / d.ksplit;
   const int kt0 = blockIdx.z * per;
@@ -263,24 +268,26 @@ __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
     _Float16* ahi = hl + buf * C::STAGE;
     _Float16* alo = ahi + C::PA;
     _Float16* bpl = ahi + C::NPL * C::PA + plane * C::PB;
+    // packed round-toward-zero split (conv_epilogue.h split_x3; measured -0.3 ms per ERes2NetV2
+    // forward against per-element round-to-nearest conversions), or the scaled split
+    {
 #pragma unroll
-    for (int r = 0; r < AROWS; ++r) {
-      const f32x4 v = al.value(st.a, r);
-      // packed round-toward-zero split (conv_epilogue.h split_x3; measured -0.3 ms per
-      // ERes2NetV2 forward against per-element round-to-nearest conversions)
-      const int off = (row0 + RPP * r) * C::LROW + kq * 4;
-      if constexpr (X1) {
-        *reinterpret_cast<f16x4*>(ahi + off) = __builtin_convertvector(v, f16x4);
-      } else {
-        f16x4 h, l;
+      for (int r = 0; r < AROWS; ++r) {
+        const f32x4 v = al.value(st.a, r);
+        const int off = (row0 + RPP * r) * C::LROW + kq * 4;
+        if constexpr (X1) {
+          *reinterpret_cast<f16x4*>(ahi + off) = __builtin_convertvector(v * sc, f16x4);
+        } else {
+          f16x4 h, l;
 #if SPK_GEXP == 2
-        h = __builtin_convertvector(v, f16x4);
-        l = h;
+          h = __builtin_convertvector(v, f16x4);
+          l = h;
 #else
-        split_x3(v, h, l);
+          split(v, h, l);
 #endif
-        *reinterpret_cast<f16x4*>(ahi + off) = h;
-        *reinterpret_cast<f16x4*>(alo + off) = l;
+          *reinterpret_cast<f16x4*>(ahi + off) = h;
+          *reinterpret_cast<f16x4*>(alo + off) = l;
+        }
       }
     }
 #pragma unroll
@@ -380,28 +387,51 @@ __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d) {
       __syncthreads();
     }
   }
-  if constexpr (!X1) {
+  {
+    const float back = pow2_div(sc, X1 ? 0 : -11);   // 2^(-11) / sc, exact
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        acc[i][j] *= (1.0f / 2048.0f);
+        acc[i][j] *= back;
   }
   epilogue_tiles<TM, TN>(d, lds, acc, wave, lane, n0 + wn * C::WTN, M, [&](int r) { return m0 + wm * C::WTM + r; });
 }
 
+// A 128-VGPR budget (4 waves per SIMD) for the <= 128x128 tiles: the in-range instance fits
+// it without spills (125 VGPRs); a budget of 256 let the compiler take 160+ VGPRs and measured
+// 16-23 % slower on every launch with more than one block per CU (ECAPA / CAM++ layers), even
+// though the 80 KB of LDS allows two blocks per CU either way.  The scaled instance spills
+// under this budget -- it runs only while the range word is set.
+#ifndef SPK_X3_LB
+#define SPK_X3_LB 4
+#endif
+// The body twice behind one uniform branch on the range word: the in-range instance is the
+// unscaled kernel exactly (a scale threaded through one shared K loop measured +25 % on the
+// 128x128 tiles: an extra VALU per value pair, and register copies of the accumulators where
+// two loop copies merged), the scaled one (common.h scaled split) runs only when the word is set.
+template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE, bool BUF, bool X1>
+__device__ __forceinline__ void conv_gemm_f16_entry(const ConvDesc& d) {
+  SPK_GATE(d.run_if);
+  __shared__ __attribute__((aligned(16))) float lds[X3Cfg<BM, BN, WM, WN, X1>::LDS_FLOATS];
+  const float sc = range_scale(d.range_in);
+  if (sc == 1.0f) conv_gemm_f16_body<BM, BN, WM, WN, S1, ADD, PRE, BUF, X1, false>(d, lds, 1.0f);
+  else conv_gemm_f16_body<BM, BN, WM, WN, S1, ADD, PRE, BUF, X1, true>(d, lds, sc);
+}
+
 template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE, bool BUF>
-__global__ void __launch_bounds__(64 * WM * WN, (BM * BN <= 128 * 128) ? 4 : 1)
+__global__ void __launch_bounds__(64 * WM * WN, (BM * BN <= 128 * 128) ? SPK_X3_LB : 1)
 conv_gemm_x3_kernel(const ConvDesc d) {
-  conv_gemm_f16_body<BM, BN, WM, WN, S1, ADD, PRE, BUF, false>(d);
+  conv_gemm_f16_entry<BM, BN, WM, WN, S1, ADD, PRE, BUF, false>(d);
 }
 
 template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE>
 __global__ void __launch_bounds__(64 * WM * WN, (BM * BN <= 128 * 128) ? 2 : 1)
 conv_gemm_x1_kernel(const ConvDesc d) {
-  conv_gemm_f16_body<BM, BN, WM, WN, S1, ADD, PRE, true, true>(d);
+  conv_gemm_f16_entry<BM, BN, WM, WN, S1, ADD, PRE, true, true>(d);
 }
 
+#ifndef SPK_CG_PART
 // Split-K combine: out = epi(sum_z partial[z])   (fixed z order: deterministic)
 __global__ void splitk_reduce_kernel(const ConvDesc d, int M) {
   SPK_GATE(d.run_if);
@@ -417,9 +447,11 @@ __global__ void splitk_reduce_kernel(const ConvDesc d, int M) {
   }
   range_note(d.range_flag, amax);
 }
+#endif
 
 }  // namespace
 
+#ifndef SPK_CG_PART
 // split-K combine of the partial slabs a GEMM launch left in d.partial (ksplit > 1)
 hipError_t launch_splitk_reduce(const ConvDesc& d, hipStream_t s) {
   const int M = d.nimg * d.Ho * d.Wo;
@@ -428,6 +460,7 @@ hipError_t launch_splitk_reduce(const ConvDesc& d, hipStream_t s) {
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(rb), dim3(256), 0, s, d, M);
   return hipGetLastError();
 }
+#endif
 
 namespace {
 
@@ -481,51 +514,102 @@ Cfg select_cfg(const ConvDesc& d) {
   return {128, 128, 32, 2, 4};
 }
 
-template <int BM, int BN, int BK, int WM, int WN>
-hipError_t launch_cfg(const ConvDesc& d, hipStream_t s) {
+// the fp16x3 / fp16 kernels of one tile (launch_tile decides that they apply: f16_path)
+template <int BM, int BN, int WM, int WN>
+hipError_t launch_f16(const ConvDesc& d, hipStream_t s) {
   const int M = d.nimg * d.Ho * d.Wo;
   const int nblk = ((M + BM - 1) / BM) * ((d.N + BN - 1) / BN);
   dim3 grid(nblk, 1, d.ksplit);
   dim3 block(64 * WM * WN);
   const bool s1 = d.s1.p != nullptr, add = d.s0.p2 != nullptr, pre = d.s0.pre_scale != nullptr;
-  if ((int)s1 + (int)add + (int)pre > 1) return hipErrorInvalidValue;
   if (d.x1 && d.wh && conv_buf_loader_ok(d, BM)) {
     if (s1) hipLaunchKernelGGL((conv_gemm_x1_kernel<BM, BN, WM, WN, true, false, false>), grid, block, 0, s, d);
     else if (add) hipLaunchKernelGGL((conv_gemm_x1_kernel<BM, BN, WM, WN, false, true, false>), grid, block, 0, s, d);
     else if (pre) hipLaunchKernelGGL((conv_gemm_x1_kernel<BM, BN, WM, WN, false, false, true>), grid, block, 0, s, d);
     else hipLaunchKernelGGL((conv_gemm_x1_kernel<BM, BN, WM, WN, false, false, false>), grid, block, 0, s, d);
-  } else if (use_x3() && d.wh && d.wl && !d.wbig) {
-    if (conv_buf_loader_ok(d, BM)) {
-      if (s1) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, true, false, false, true>), grid, block, 0, s, d);
-      else if (add) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, true, false, true>), grid, block, 0, s, d);
-      else if (pre) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, false, true, true>), grid, block, 0, s, d);
-      else hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, false, false, true>), grid, block, 0, s, d);
-    } else if (s1 || pre) {
-      return hipErrorInvalidValue;   // no generic-loader instantiation (conv_buf_loader_ok)
-    } else if (add) {
-      hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, true, false, false>), grid, block, 0, s, d);
-    } else {
-      hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, false, false, false>), grid, block, 0, s, d);
-    }
-  } else if (s1) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, true, false, false>), grid, block, 0, s, d);
+  } else if (conv_buf_loader_ok(d, BM)) {
+    if (s1) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, true, false, false, true>), grid, block, 0, s, d);
+    else if (add) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, true, false, true>), grid, block, 0, s, d);
+    else if (pre) hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, false, true, true>), grid, block, 0, s, d);
+    else hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, false, false, true>), grid, block, 0, s, d);
+  } else if (s1 || pre) {
+    return hipErrorInvalidValue;   // no generic-loader instantiation (conv_buf_loader_ok)
+  } else if (add) {
+    hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, true, false, false>), grid, block, 0, s, d);
+  } else {
+    hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN, WM, WN, false, false, false, false>), grid, block, 0, s, d);
+  }
+  return hipGetLastError();
+}
+
+// the exact fp32 MFMA kernels of one tile
+template <int BM, int BN, int BK, int WM, int WN>
+hipError_t launch_f32(const ConvDesc& d, hipStream_t s) {
+  const int M = d.nimg * d.Ho * d.Wo;
+  const int nblk = ((M + BM - 1) / BM) * ((d.N + BN - 1) / BN);
+  dim3 grid(nblk, 1, d.ksplit);
+  dim3 block(64 * WM * WN);
+  const bool s1 = d.s1.p != nullptr, add = d.s0.p2 != nullptr, pre = d.s0.pre_scale != nullptr;
+  if (s1) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, true, false, false>), grid, block, 0, s, d);
   else if (add) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, false, true, false>), grid, block, 0, s, d);
   else if (pre) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, false, false, true>), grid, block, 0, s, d);
   else hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, WM, WN, false, false, false>), grid, block, 0, s, d);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || d.ksplit <= 1) return e;
-  return launch_splitk_reduce(d, s);
+  return hipGetLastError();
 }
 
 template <int BK>
-hipError_t launch_bk(const ConvDesc& d, const Cfg& c, hipStream_t s) {
-  if (c.bn == 32) return launch_cfg<256, 32, BK, 8, 1>(d, s);
-  if (c.bn == 64) return launch_cfg<256, 64, BK, 4, 2>(d, s);
-  if (c.bm == 64) return launch_cfg<64, 128, BK, 1, 4>(d, s);
-  if (c.bm == 256) return launch_cfg<256, 128, BK, 4, 2>(d, s);
-  if (c.bn == 256) return launch_cfg<128, 256, BK, 2, 4>(d, s);
-  return launch_cfg<128, 128, BK, 2, 4>(d, s);
+hipError_t launch_f32_bk(const ConvDesc& d, int bm, int bn, hipStream_t s) {
+  if (bn == 32) return launch_f32<256, 32, BK, 8, 1>(d, s);
+  if (bn == 64) return launch_f32<256, 64, BK, 4, 2>(d, s);
+  if (bm == 64) return launch_f32<64, 128, BK, 1, 4>(d, s);
+  if (bm == 256) return launch_f32<256, 128, BK, 4, 2>(d, s);
+  if (bn == 256) return launch_f32<128, 256, BK, 2, 4>(d, s);
+  return launch_f32<128, 128, BK, 2, 4>(d, s);
 }
 
+}  // namespace
+
+// Build split: the launch paths (their kernel instantiations are most of this file's compile
+// time, the fp16x3 ones doubled by the scaled-split instances) are compiled from this file as
+// four more objects, -DSPK_CG_PART=0..3 (Makefile), in parallel; the part-less object holds the
+// dispatch below and calls them.
+hipError_t conv_launch_part0(const ConvDesc& d, hipStream_t s, int bm, int bn);   // f16: 128x128
+hipError_t conv_launch_part1(const ConvDesc& d, hipStream_t s, int bm, int bn);   // f16: 256x128, 128x256
+hipError_t conv_launch_part2(const ConvDesc& d, hipStream_t s, int bm, int bn);   // f16: 256x32, 256x64, 64x128
+hipError_t conv_launch_part3(const ConvDesc& d, hipStream_t s, int bm, int bn, int bk);   // exact fp32, all tiles
+
+#if defined(SPK_CG_PART) && SPK_CG_PART == 0
+hipError_t conv_launch_part0(const ConvDesc& d, hipStream_t s, int, int) { return launch_f16<128, 128, 2, 4>(d, s); }
+#elif defined(SPK_CG_PART) && SPK_CG_PART == 1
+hipError_t conv_launch_part1(const ConvDesc& d, hipStream_t s, int bm, int) {
+  return bm == 256 ? launch_f16<256, 128, 4, 2>(d, s) : launch_f16<128, 256, 2, 4>(d, s);
+}
+#elif defined(SPK_CG_PART) && SPK_CG_PART == 2
+hipError_t conv_launch_part2(const ConvDesc& d, hipStream_t s, int, int bn) {
+  if (bn == 32) return launch_f16<256, 32, 8, 1>(d, s);
+  if (bn == 64) return launch_f16<256, 64, 4, 2>(d, s);
+  return launch_f16<64, 128, 1, 4>(d, s);
+}
+#elif defined(SPK_CG_PART) && SPK_CG_PART == 3
+hipError_t conv_launch_part3(const ConvDesc& d, hipStream_t s, int bm, int bn, int bk) {
+  return bk == 32 ? launch_f32_bk<32>(d, bm, bn, s) : launch_f32_bk<16>(d, bm, bn, s);
+}
+#endif
+
+#ifndef SPK_CG_PART
+namespace {
+hipError_t launch_tile(const ConvDesc& d, const Cfg& c, hipStream_t s) {
+  const bool s1 = d.s1.p != nullptr, add = d.s0.p2 != nullptr, pre = d.s0.pre_scale != nullptr;
+  if ((int)s1 + (int)add + (int)pre > 1) return hipErrorInvalidValue;
+  const bool f16 = (d.x1 && d.wh && conv_buf_loader_ok(d, c.bm)) || (use_x3() && d.wh && d.wl && !d.wbig);
+  hipError_t e;
+  if (!f16) e = conv_launch_part3(d, s, c.bm, c.bn, c.bk);
+  else if (c.bn == 32 || c.bn == 64 || c.bm == 64) e = conv_launch_part2(d, s, c.bm, c.bn);
+  else if (c.bm == 256 || c.bn == 256) e = conv_launch_part1(d, s, c.bm, c.bn);
+  else e = conv_launch_part0(d, s, c.bm, c.bn);
+  if (e != hipSuccess || d.ksplit <= 1) return e;
+  return launch_splitk_reduce(d, s);
+}
 }  // namespace
 
 // Name of the kernel instantiation launch_conv() picks (matches rocprofv3 kernel names).
@@ -567,8 +651,8 @@ hipError_t launch_conv(const ConvDesc& dd, hipStream_t s) {
   if (halo_conv_supported(d)) return launch_conv3x3_halo(d, s);
   if (use_x3() && pw_supported(d)) return launch_pw(d, s);
   if (use_x3() && gemm_f_supported(d)) return launch_gemm_f(d, s);
-  const Cfg c = select_cfg(d);
-  return c.bk == 32 ? launch_bk<32>(d, c, s) : launch_bk<16>(d, c, s);
+  return launch_tile(d, select_cfg(d), s);
 }
+#endif  // !SPK_CG_PART
 
 }  // namespace spk

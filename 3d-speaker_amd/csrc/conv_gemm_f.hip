@@ -118,6 +118,7 @@ template <int BM, int BN, int WM, int WN, int OP2>
 __global__ void __launch_bounds__(64 * WM * WN, (FCfg<BM, BN, WM, WN>::WAVES_PER_EU))
 conv_gemm_x3f_kernel(const ConvDesc d) {
   SPK_GATE(d.run_if);
+  const float sc = range_scale(d.range_in);            // scaled split: operand x 2^-s (common.h)
   using C = FCfg<BM, BN, WM, WN>;
   constexpr bool ADD = OP2 == 1, S1 = OP2 == 2;
   constexpr int TM = C::TM, TN = C::TN, ROWS = C::ROWS, NT = C::NT;
@@ -243,19 +244,21 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
       tdpB = kyB * dyW + kxB * dx;
     }
   };
-  auto store_a = [&](int buf, const ASet& s) {
+  auto store_a = [&](int buf, const ASet& s, auto split) {
     if ((SPK_FEXP & 4) && inloop) return;
     _Float16* ahi = reinterpret_cast<_Float16*>(lb + buf * C::STAGE);
     _Float16* alo = ahi + C::PA;
+    {
 #pragma unroll
-    for (int r = 0; r < ROWS; ++r) {
-      f32x4 v = s.v[r];
-      if (OP2) v += s.v2[r];                           // addend, or s1 (exactly one of the two is nonzero)
-      f16x4 h, l;
-      split_x3(v, h, l);
-      const int off = (row0 + RPP * r) * C::LROW + kq * 4;
-      *reinterpret_cast<f16x4*>(ahi + off) = h;
-      *reinterpret_cast<f16x4*>(alo + off) = l;
+      for (int r = 0; r < ROWS; ++r) {
+        f32x4 v = s.v[r];
+        if (OP2) v += s.v2[r];                         // addend, or s1 (exactly one of the two is nonzero)
+        f16x4 h, l;
+        split(v, h, l);
+        const int off = (row0 + RPP * r) * C::LROW + kq * 4;
+        *reinterpret_cast<f16x4*>(ahi + off) = h;
+        *reinterpret_cast<f16x4*>(alo + off) = l;
+      }
     }
   };
 
@@ -312,6 +315,10 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
   // `break` between the steps it merged two states and waited vmcnt(0) at the top).  Every
   // load and DMA in the loop is unconditional (clamped past the end: zeros, or a re-read of
   // the last tile into the idle buffer), so the body has no branch around a memory operation.
+  // The whole K loop twice behind one uniform branch: the plain split while the range word is
+  // clear, the scaled split (common.h) otherwise (a branch in the loop body would split the
+  // basic block the sched_barrier placement relies on).
+  split_pass(sc, [&](auto split) {
   if (C::ONE_SET && kt0 < kt1) {
     // one A register set (the 256 x 256 tile, whose accumulators take half the registers):
     // the loads of K-tile kt + 1 are issued right after the stores of kt, so they have the
@@ -319,7 +326,7 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
     ASet set;
     dma_b(kt0, 0);
     load_a(set);
-    store_a(0, set);
+    store_a(0, set, split);
     load_a(set);                                       // kt0 + 1
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALOADS) : "memory");   // B of kt0 landed
     __syncthreads();
@@ -335,7 +342,7 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
       // the gaps of the second k-step's MFMAs
       compute_s(buf, 0);
       __builtin_amdgcn_sched_barrier(0);
-      store_a(buf ^ 1, set);
+      store_a(buf ^ 1, set, split);
       load_a(set);
       compute_s(buf, 1);
 #else
@@ -343,7 +350,7 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
       // keep the split of the A set (loaded at the end of the previous step) behind the MFMAs:
       // hoisted to the top of the step it waited for those loads before any MFMA could issue
       __builtin_amdgcn_sched_barrier(0);
-      store_a(buf ^ 1, set);                           // K-tile kt + 1 (past the end: unused)
+      store_a(buf ^ 1, set, split);                    // K-tile kt + 1 (past the end: unused)
       load_a(set);                                     // kt + 2
 #endif
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALOADS) : "memory");   // B of kt + 1 landed
@@ -357,7 +364,7 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
     dma_b(kt0, 0);
     load_a(set0);
     load_a(set1);                                      // kt0 + 1 (or past the end: unused)
-    store_a(0, set0);
+    store_a(0, set0, split);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALOADS) : "memory");   // B of kt0 landed
     __syncthreads();
     inloop = true;
@@ -369,12 +376,12 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
 #if SPK_F_SCHED & 4
       compute_s(0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      store_a(1, set1);
+      store_a(1, set1, split);
       compute_s(0, 1);
 #else
       compute(0);
       __builtin_amdgcn_sched_barrier(0);
-      store_a(1, set1);
+      store_a(1, set1, split);
 #endif
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALOADS) : "memory");   // B of kt + 1 landed
       __syncthreads();
@@ -384,12 +391,12 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
 #if SPK_F_SCHED & 4
       compute_s(1, 0);
       __builtin_amdgcn_sched_barrier(0);
-      store_a(0, set0);
+      store_a(0, set0, split);
       compute_s(1, 1);
 #else
       compute(1);
       __builtin_amdgcn_sched_barrier(0);
-      store_a(0, set0);
+      store_a(0, set0, split);
 #endif
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ALOADS) : "memory");
       __syncthreads();
@@ -399,10 +406,12 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
       __syncthreads();                                 // the epilogue reuses the LDS
     }
   }
+  });
+  const float back = pow2_div(sc, -11);               // 2^(-11) / sc, exact
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] *= (1.0f / 2048.0f);
+    for (int j = 0; j < TN; ++j) acc[i][j] *= back;
 #if SPK_FEXP & 16
   if (acc[0][0][0] == 1234.5f && acc[TM - 1][TN - 1][3] == 77.f) d.out[tid] = acc[0][0][1];
 #else

@@ -50,6 +50,8 @@ template <int KP, int BN, bool S1, bool RES>
 __global__ void __launch_bounds__(512, 1)
 pw_gemm_x3_kernel(const ConvDesc d) {
   SPK_GATE(d.run_if);
+  // scaled split (common.h): operand x 2^-s at staging, accumulators x 2^s in the epilogue
+  const float sc = range_scale(d.range_in), back = pow2_div(sc, 0), back_x = pow2_div(sc, -11);
   using C = PwCfg<KP, BN>;
   __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
   _Float16* Bh = reinterpret_cast<_Float16*>(lds);
@@ -111,16 +113,18 @@ pw_gemm_x3_kernel(const ConvDesc d) {
     }
   };
   auto store_a = [&](const f32x4 (&v)[C::AQ]) {
+    split_pass(sc, [&](auto split) {                       // scaled split (common.h) when the word is set
 #pragma unroll
-    for (int i = 0; i < C::AQ; ++i) {
-      const int idx = tid + C::NT * i;
-      const int row = idx / C::QR, q = idx % C::QR;
-      const bool kin = 4 * q < K;                          // K padding columns are zero
-      f16x4 h, l;
-      split_x3(kin ? v[i] : f32x4{0.f, 0.f, 0.f, 0.f}, h, l);
-      *reinterpret_cast<f16x4*>(Ah + row * C::LROW + 4 * q) = h;
-      *reinterpret_cast<f16x4*>(Al + row * C::LROW + 4 * q) = l;
-    }
+      for (int i = 0; i < C::AQ; ++i) {
+        const int idx = tid + C::NT * i;
+        const int row = idx / C::QR, q = idx % C::QR;
+        const bool kin = 4 * q < K;                        // K padding columns are zero
+        f16x4 h, l;
+        split(kin ? v[i] : f32x4{0.f, 0.f, 0.f, 0.f}, h, l);
+        *reinterpret_cast<f16x4*>(Ah + row * C::LROW + 4 * q) = h;
+        *reinterpret_cast<f16x4*>(Al + row * C::LROW + 4 * q) = l;
+      }
+    });
   };
 
   const int n = n0 + wn * 32 + li;                         // this lane's output column
@@ -167,7 +171,7 @@ pw_gemm_x3_kernel(const ConvDesc d) {
         for (int r = 0; r < 16; ++r) {
           const int m = mbase + (r & 3) + 8 * (r >> 2);
           if (m >= M) continue;
-          float v = acc[r] + accx[r] * (1.0f / 2048.0f) + bias + res[r];
+          float v = acc[r] * back + accx[r] * back_x + bias + res[r];
           if constexpr (A >= 0) {
             v = apply_act(v, A);
           } else {

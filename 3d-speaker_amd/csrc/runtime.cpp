@@ -217,6 +217,7 @@ void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const C
   d.wl = exact ? nullptr : m.dlo(p.w_off);
   d.wf = (exact || !m.dfrag || p.f_off == SIZE_MAX) ? nullptr : m.dfrag + p.f_off;
   const bool guard = !exact;   // producers note fp16x3 range overflows in the forward's word
+  const bool scale_in = !exact && scaled;
   d.x1 = (!exact && m.fp16 && x1_scope) ? 1 : 0;
   d.wbig = p.wmax >= kX3WeightLimit ? 1 : 0;
   d.bias = (use_bias && p.has_bias) ? m.dptr(p.b_off) : nullptr;
@@ -247,8 +248,9 @@ void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const C
   if (io.s1) bytes += 4.0 * px_out * d.s1.cin;
   if (io.res) bytes += 4.0 * px_out * d.N;
   if (io.affx) bytes += 8.0 * px_out * d.N;
-  step(name, [d, cio, guard](const Ctx& c) mutable {
+  step(name, [d, cio, guard, scale_in](const Ctx& c) mutable {
     d.range_flag = guard ? c.flag : nullptr;
+    d.range_in = scale_in ? c.flag : nullptr;
     d.s0.p = c.resolve(cio.s0);
     d.s0.p2 = c.resolve(cio.s0b);
     d.s1.p = c.resolve(cio.s1);
@@ -339,9 +341,23 @@ spk::PlanPair::~PlanPair() {
 
 namespace {
 
+// SPK_RANGE_MODE=twin: ECAPA / CAM++ keep the gated exact twin instead of the scaled split (A/B)
+static bool range_scaled() {
+  static const bool on = [] {
+    const char* e = std::getenv("SPK_RANGE_MODE");
+    return !(e && std::string(e) == "twin");
+  }();
+  return on;
+}
+
 std::unique_ptr<Plan> build_plan(spk_model_t* h, int B, int T, bool ragged, bool exact) {
   auto plan = std::make_unique<Plan>();
   Builder b(h->m, plan.get(), B, ragged, exact);
+  // ECAPA / CAM++: unbounded activations everywhere (ReLU -> BN), so the whole plan would need
+  // the exact twin; instead every split GEMM scales its operand by the range word (common.h)
+  const int arch = h->m.cfg.arch;
+  b.scaled = !exact && range_scaled() && (arch == SPK_ARCH_ECAPA || arch == SPK_ARCH_CAMPPLUS);
+  plan->scaled = b.scaled;
   if (!exact) {
     // fp16x3 range guard on the model input (common.h)
     const size_t n = (size_t)B * T * h->m.cfg.feat_dim;
@@ -670,6 +686,7 @@ static int enqueue_steps(const char* fn, const PlanPair& pp, const Ctx& base, bo
     return rc;
   }
   static const bool no_rerun = std::getenv("SPK_DIAG_NO_RERUN") != nullptr;   // diagnostics only
+  if (pp.x3->scaled) return run(*pp.x3, 0, pp.x3->steps.size(), word, nullptr);   // no twin
   if (segmented(pp)) {
     // segment by segment: a segment's exact twin, gated on the word, follows it only where one
     // of its split-GEMM operands is not statically bounded below kRangeLimit (Builder::segment);
@@ -804,6 +821,10 @@ int spk_model_guard_plan(spk_model_t* model, int32_t B, int32_t T, int32_t ragge
     std::shared_ptr<PlanPair> pp = get_pair(model, B, T, ragged != 0);
     *n_segments = *n_twin_segments = *n_gated_steps = 0;
     if (!pp->x3) return SPK_OK;
+    if (pp->x3->scaled) {   // scaled split: one segment, nothing gated behind it
+      *n_segments = 1;
+      return SPK_OK;
+    }
     if (!segmented(*pp)) {
       *n_segments = *n_twin_segments = 1;
       *n_gated_steps = (int32_t)pp->ex->steps.size();

@@ -65,6 +65,9 @@ struct Plan {
   // so the runtime can check that both plans of a pair place every buffer alike
   std::vector<size_t> seg_end;
   std::vector<char> seg_twin;
+  // scaled split (common.h): every split GEMM of the plan scales its operand by the range
+  // word, so a set word needs no exact twin (ECAPA, CAM++)
+  bool scaled = false;
   std::vector<std::pair<size_t, size_t>> allocs;
 };
 
@@ -174,6 +177,8 @@ struct Builder {
   double macs_at_last_step = 0;
   bool ragged = false;       // per-utterance lengths (Buf::LEN) mask the time axis
   bool exact = false;        // exact-fp32 MFMA kernels only (no fp16x3 split anywhere)
+  bool scaled = false;       // scaled split: convs read the range word for their operand scale
+                             // (common.h), the plan has no exact twin
   bool x1_scope = true;      // SPK_PRECISION_FP16 handles: convs emitted while set use the
                              // single-product kernels (model builders keep the input-side
                              // layers, whose error the network amplifies most, fp16x3)

@@ -363,9 +363,9 @@ class NativeModel:
         return out
 
     @property
-    def last_forward_exact(self) -> bool:
-        """Whether the last forward was recomputed on the exact-fp32 kernels because an
-        activation reached fp16's range (synchronises that forward's stream; diagnostics)."""
+    def last_forward_flagged(self) -> bool:
+        """Whether an activation of the last forward reached the fp16x3 range limit (its range
+        word is set; synchronises that forward's stream; diagnostics)."""
         if self._last is None:
             return False
         B, T, ragged, ws, stream = self._last
@@ -374,6 +374,16 @@ class NativeModel:
             _check(lib().spk_model_range_check(self.handle, B, T, ragged, ws.data_ptr(), stream, ctypes.byref(flag)),
                    'spk_model_range_check')
         return bool(flag.value)
+
+    @property
+    def last_forward_exact(self) -> bool:
+        """Whether the last forward was recomputed on the exact-fp32 kernels because an
+        activation reached fp16's range: its word is set and its plan has an exact twin
+        (ECAPA / CAM++ plans scale the split operands instead and have none)."""
+        if not self.last_forward_flagged:
+            return False
+        B, T, ragged = self._last[:3]
+        return self.guard_plan(B, T, bool(ragged))['twin_segments'] > 0
 
     def guard_plan(self, B: int, T: int, ragged: bool = False) -> dict:
         """How the guarded forward of shape (B, T) is cut into range-guard segments and how

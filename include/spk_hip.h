@@ -142,14 +142,15 @@ int spk_model_forward_lengths(spk_model_t* model, const float* feats, int32_t B,
 /* fp16x3 range guard, resolved on the device.  The default kernels represent every GEMM
  * operand as two fp16 values (fp32-accurate, csrc/conv_gemm.hip); a value at or past fp16's
  * range (65504) would saturate.  Every producer of an unbounded activation (and the input
- * check) sets a range word in the caller's workspace -- one per forward, zeroed when the
- * forward starts -- when a value reaches 2^14; the forward then re-runs itself on exact-fp32
- * MFMA kernels, launched behind it on the same stream and gated on that word, and the exact
- * embeddings replace the split ones.  spk_model_forward* therefore only enqueue (no host
- * synchronisation), and concurrent forwards on different streams with different workspaces
- * never see each other's word.  spk_model_range_check() reports (synchronising `stream`)
- * whether the last forward of shape (B, T, ragged) that used `workspace` took the exact
- * re-run (diagnostics).  spk_model_forward_exact() (same arguments as
+ * check) raises a range word in the caller's workspace -- one per forward, zeroed when the
+ * forward starts -- to the largest value it wrote once that reaches 2^14.  ECAPA-TDNN and
+ * CAM++ GEMMs then split their operands scaled by a power of two taken from the word (exact,
+ * no re-run); ERes2Net* / ResNet re-run the flagged plan segment on exact-fp32 MFMA kernels,
+ * launched behind it on the same stream and gated on that word.  spk_model_forward* therefore
+ * only enqueue (no host synchronisation), and concurrent forwards on different streams with
+ * different workspaces never see each other's word.  spk_model_range_check() reports
+ * (synchronising `stream`) whether the word of the last forward of shape (B, T, ragged) that
+ * used `workspace` was set (diagnostics).  spk_model_forward_exact() (same arguments as
  * spk_model_forward_lengths, lengths may be NULL) runs the exact plan only.  A handle whose
  * packed weights leave fp16's range always runs exact.  The workspace queries cover both
  * plans. */
@@ -160,10 +161,11 @@ int spk_model_forward_exact(spk_model_t* model, const float* feats, int32_t B, i
 /* How the guarded forward of shape (B, T, ragged) is cut (diagnostics, tests): the exact
  * re-run is captured per segment of the plan, right behind the segment it can replace, and
  * only for segments with a split-GEMM operand not statically bounded below 2^14 (ERes2Net*:
- * Hardtanh / weight-norm bounds leave only the stem's segment; other models: one segment,
- * the whole plan).  n_segments: segments of the plan; n_twin_segments: those with an exact
- * twin; n_gated_steps: launches of the exact plan enqueued behind every guarded forward
- * (no-ops unless the range word is set); 0 / 0 / 0 for an exact-only handle. */
+ * Hardtanh / weight-norm bounds leave only the stem's segment; ResNet: one segment, the whole
+ * plan; ECAPA-TDNN / CAM++: scaled split, one segment, no twin).  n_segments: segments of the
+ * plan; n_twin_segments: those with an exact twin; n_gated_steps: launches of the exact plan
+ * enqueued behind every guarded forward (no-ops unless the range word is set); 0 / 0 / 0 for
+ * an exact-only handle. */
 int spk_model_guard_plan(spk_model_t* model, int32_t B, int32_t T, int32_t ragged, int32_t* n_segments,
                          int32_t* n_twin_segments, int32_t* n_gated_steps);
 

@@ -56,6 +56,15 @@ static float epilogue(const ConvDesc& d, int m, int n, float v) {
   return row_masked(d, m) ? 0.f : v;
 }
 
+static void emu_range_note(int* flag, float v) {   // common.h range guard: max of the float bits
+  const float a = std::fabs(v);
+  if (flag && a >= kRangeLimit) {
+    int bits;
+    std::memcpy(&bits, &a, sizeof(bits));
+    if (bits > *flag) *flag = bits;
+  }
+}
+
 hipError_t launch_conv(const ConvDesc& d, hipStream_t) {
   EMU_GATE();
   if (d.s0.cin % 4 || d.s0.ld % 4 || d.Kp % 16 || (d.osplit ? (d.osplit % 4 || d.ldo < d.osplit) : d.ldo < d.N) || d.K > d.Kp) return hipErrorInvalidValue;
@@ -97,7 +106,7 @@ hipError_t launch_conv(const ConvDesc& d, hipStream_t) {
       for (int k = 0; k < d.Kp; ++k) acc += (double)a[k] * w[k];
       {
         const float o = epilogue(d, m, n, (float)acc);
-        if (d.range_flag && std::fabs(o) >= kRangeLimit) *d.range_flag |= 1;
+        emu_range_note(d.range_flag, o);
         *out_at(d, m, n) = o;
       }
     }
@@ -143,9 +152,6 @@ hipError_t launch_split_f16(const float*, uint16_t*, uint16_t*, size_t, hipStrea
 size_t frag_halves(int N, int Kp) { return (size_t)Kp * (size_t)((N + 255) / 256 * 256) * 2; }
 hipError_t launch_pack_frag(const uint16_t*, const uint16_t*, int, int, uint16_t*, hipStream_t) { return hipSuccess; }
 
-static void emu_range_note(int* flag, float v) {   // common.h range guard
-  if (flag && std::fabs(v) >= kRangeLimit) *flag |= 1;
-}
 
 hipError_t launch_word_reset(int* w, hipStream_t) {
   *w = 0;

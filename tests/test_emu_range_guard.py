@@ -1,7 +1,8 @@
 """fp16x3 range guard plumbing on the host emulation (tests/emu): a model whose activations
-reach the range limit raises the forward's range word (a workspace slot), the gated exact
-plan captured behind the split one then recomputes the batch (the forward's output
-reproduces the oracle), the word belongs to its workspace (two interleaved forwards with two
+reach the range limit raises the forward's range word (a workspace slot), the forward still
+reproduces the oracle (ERes2Net: the gated exact twin of the flagged segment recomputes it;
+ECAPA / CAM++: the split GEMMs scale their operands by the word -- the emulated GEMMs are
+exact, so here only the plumbing is checked), the word belongs to its workspace (two interleaved forwards with two
 workspaces do not see each other's), spk_model_forward_exact runs the exact plan alone, and
 weights past fp16's range force the exact path at creation.  The GPU test
 (tests/test_gpu_range_guard.py) checks the kernels."""
@@ -54,7 +55,7 @@ def test_large_activations_flag_and_exact_path():
     assert _flag(em) == 1                                       # reading does not clear it
     ref = models_ref.forward('ecapa', {k: v.double() if v.is_floating_point() else v
                                        for k, v in m.state_dict().items()}, feats.double()).numpy()
-    assert helpers.rel_err(guarded, ref).max() < 1e-4           # the gated exact re-run ran
+    assert helpers.rel_err(guarded, ref).max() < 1e-4
     out = _forward_exact(em, feats).numpy()
     assert helpers.rel_err(out, ref).max() < 1e-4
 
@@ -141,10 +142,10 @@ def test_eres2net_hot_input_reruns_the_stem_segment():
     assert helpers.rel_err(out, ref).max() < 1e-4
 
 
-def test_unbounded_models_keep_one_twinned_segment():
-    """ECAPA / CAM++ activations are unbounded (ReLU -> BN): the whole exact plan stays gated
-    behind the whole split plan."""
+def test_unbounded_models_scale_instead_of_twin():
+    """ECAPA / CAM++ activations are unbounded (ReLU -> BN): their split GEMMs scale the operand
+    by the range word (common.h scaled split), so nothing is gated behind the plan."""
     for arch in ('ecapa', 'campplus'):
         em = EmuModel(helpers.loaded_module(arch))
         nseg, ntwin, ngated = _guard_plan(em, 1, 40)
-        assert nseg == 1 and ntwin == 1 and ngated > 20
+        assert nseg == 1 and ntwin == 0 and ngated == 0

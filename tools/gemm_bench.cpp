@@ -38,6 +38,7 @@ struct Shape {
   bool res;
   int addend;   // Res2Net addend operand (s0.p2)
   int s1cin = 0, s1H = 0, s1W = 0, s1s = 1;   // K-concatenated 1x1 operand (projection shortcut)
+  int oned = 0, dil = 1, reflect = 0, pre = 0;   // 1-D (TDNN) conv over W, dilation, reflect pad, BN-ReLU pre-activation
 };
 
 // ERes2NetV2 (m_channels 64, baseWidth 26, scale 2, expansion 2) at B = 256, T = 198
@@ -54,6 +55,12 @@ static const Shape kShapes[] = {
     {"l2.0.conv3", 256, 40, 99, 104, 256, 1, 1, ACT_HTANH, false, 0, 128, 80, 198, 2},
     {"l3.0.conv3", 256, 20, 50, 208, 512, 1, 1, ACT_HTANH, false, 0, 256, 40, 99, 2},
     {"fuse34.att0", 256, 10, 25, 1024, 256, 1, 1, ACT_SILU, false, 0, 1024, 10, 25, 1},
+    // ECAPA-TDNN (C=1024) and CAM++ layers at B = 256, T = 198 on the tiled fp16x3 GEMM
+    {"ec.b0", 256, 1, 198, 80, 1024, 5, 1, ACT_RELU, false, 0, 0, 0, 0, 1, 1, 1, 1, 0},
+    {"ec.r2n", 256, 1, 198, 128, 128, 3, 1, ACT_RELU, false, 1, 0, 0, 0, 1, 1, 2, 1, 0},
+    {"ec.tdnn1", 256, 1, 198, 1024, 1024, 1, 1, ACT_RELU, false, 0, 0, 0, 0, 1, 1, 1, 1, 0},
+    {"cam.transit", 256, 1, 99, 512, 256, 1, 1, ACT_NONE, false, 0, 0, 0, 0, 1, 1, 1, 0, 1},
+    {"cam.linear1", 256, 1, 99, 256, 128, 1, 1, ACT_NONE, false, 0, 0, 0, 0, 1, 1, 1, 0, 1},
 };
 
 struct Lib {
@@ -90,10 +97,12 @@ int main(int argc, char** argv) {
 
   for (const Shape& sh : kShapes) {
     if (!only.empty() && ("," + only + ",").find(std::string(",") + sh.name + ",") == std::string::npos) continue;
-    const int pad = sh.k / 2;
-    const int Ho = (sh.H + 2 * pad - sh.k) / sh.s + 1, Wo = (sh.W + 2 * pad - sh.k) / sh.s + 1;
+    const int kh = sh.oned ? 1 : sh.k, pad = sh.dil * (sh.k / 2), padh = sh.oned ? 0 : pad;
+    const int Ho = sh.oned ? 1 : (sh.H + 2 * pad - sh.k) / sh.s + 1;
+    const int Wo = (sh.W + 2 * pad - sh.dil * (sh.k - 1) - 1) / sh.s + 1;
     const int M = sh.nimg * Ho * Wo;
-    const int taps = sh.k * sh.k, K0 = taps * sh.cin, K = K0 + sh.s1cin, Kp = round_up(K, 32);
+    const int taps = kh * sh.k, K0 = taps * sh.cin, K = K0 + sh.s1cin, Kp = round_up(K, 32);
+    std::vector<float> ps(sh.pre ? sh.cin : 0), pt(sh.pre ? sh.cin : 0);
     const size_t nin = (size_t)sh.nimg * sh.H * sh.W * sh.cin;
     const size_t nin1 = (size_t)sh.nimg * sh.s1H * sh.s1W * sh.s1cin;
     std::vector<float> x(nin), x2(sh.addend ? nin : 0), w((size_t)sh.N * Kp, 0.f), b(sh.N), r(sh.res ? (size_t)M * sh.N : 0);
@@ -107,6 +116,15 @@ int main(int argc, char** argv) {
       for (int k = 0; k < K; ++k) w[(size_t)n * Kp + k] = uw(rng) * ws;
     for (auto& v : b) v = uw(rng) * 0.1f;
     for (auto& v : r) v = ua(rng);
+    for (auto& v : ps) v = 0.5f + 0.5f * ua(rng);
+    for (auto& v : pt) v = uw(rng);
+    float *dps = nullptr, *dpt = nullptr;
+    if (sh.pre) {
+      CK(hipMalloc(&dps, ps.size() * 4));
+      CK(hipMalloc(&dpt, pt.size() * 4));
+      CK(hipMemcpy(dps, ps.data(), ps.size() * 4, hipMemcpyHostToDevice));
+      CK(hipMemcpy(dpt, pt.data(), pt.size() * 4, hipMemcpyHostToDevice));
+    }
     float *dx, *dx2 = nullptr, *dx1 = nullptr, *dw, *db, *dr = nullptr, *dout;
     if (nin1) {
       CK(hipMalloc(&dx1, nin1 * 4));
@@ -130,7 +148,8 @@ int main(int argc, char** argv) {
     ConvDesc d;
     d.s0.p = dx; d.s0.p2 = dx2; d.s0.ld = sh.cin; d.s0.ld2 = sh.addend ? sh.cin : 0;
     d.s0.H = sh.H; d.s0.W = sh.W; d.s0.cin = sh.cin;
-    d.s0.kh = d.s0.kw = sh.k; d.s0.sh = d.s0.sw = sh.s; d.s0.ph = d.s0.pw = pad;
+    d.s0.kh = kh; d.s0.kw = sh.k; d.s0.sh = d.s0.sw = sh.s; d.s0.ph = padh; d.s0.pw = pad;
+    d.s0.dw = sh.dil; d.s0.reflect = sh.reflect; d.s0.pre_scale = dps; d.s0.pre_shift = dpt;
     d.nimg = sh.nimg; d.Ho = Ho; d.Wo = Wo; d.N = sh.N; d.K = K; d.Kp = Kp;
     d.w = dw; d.wh = dwh; d.wl = dwl; d.bias = db; d.out = dout; d.ldo = sh.N; d.act = sh.act;
     d.res = dr; d.ldr = sh.res ? sh.N : 0;
@@ -148,14 +167,17 @@ int main(int argc, char** argv) {
       const int m = sm[i], n = sn[i];
       const int wo = m % Wo, ho = (m / Wo) % Ho, img = m / (Wo * Ho);
       double acc = b[n], a = std::fabs(b[n]);
-      for (int ky = 0; ky < sh.k; ++ky)
+      for (int ky = 0; ky < kh; ++ky)
         for (int kx = 0; kx < sh.k; ++kx) {
-          const int hi = ho * sh.s - pad + ky, wi = wo * sh.s - pad + kx;
+          const int hi = ho * sh.s - padh + ky;
+          int wi = wo * sh.s - pad + kx * sh.dil;
+          if (sh.reflect) wi = wi < 0 ? -wi : wi >= sh.W ? 2 * (sh.W - 1) - wi : wi;
           if (hi < 0 || hi >= sh.H || wi < 0 || wi >= sh.W) continue;
           const size_t px = ((size_t)img * sh.H + hi) * sh.W + wi;
           for (int c = 0; c < sh.cin; ++c) {
             double xv = x[px * sh.cin + c];
             if (sh.addend) xv += x2[px * sh.cin + c];
+            if (sh.pre) xv = std::max((double)(float)(x[px * sh.cin + c] * ps[c] + pt[c]), 0.0);
             const double p = xv * w[(size_t)n * Kp + (ky * sh.k + kx) * sh.cin + c];
             acc += p;
             a += std::fabs(p);
@@ -171,6 +193,7 @@ int main(int argc, char** argv) {
       }
       if (sh.res) { acc += r[(size_t)m * sh.N + n]; a += std::fabs(r[(size_t)m * sh.N + n]); }
       if (sh.act == ACT_HTANH) acc = std::min(std::max(acc, 0.0), 20.0);
+      if (sh.act == ACT_RELU) acc = std::max(acc, 0.0);
       if (sh.act == ACT_SILU) {
         const double a0 = a;
         acc = acc / (1.0 + std::exp(-acc));
@@ -221,6 +244,7 @@ int main(int argc, char** argv) {
     }
     CK(hipFree(dx)); if (dx2) CK(hipFree(dx2)); if (dx1) CK(hipFree(dx1)); CK(hipFree(dw)); CK(hipFree(dwh)); CK(hipFree(dwl)); CK(hipFree(db));
     if (dr) CK(hipFree(dr)); CK(hipFree(dout));
+    if (dps) CK(hipFree(dps)); if (dpt) CK(hipFree(dpt));
   }
   return 0;
 }
