@@ -738,6 +738,11 @@ static int run_graph(const char* fn, spk_model_t* model, PlanPair& pp, const flo
     if (rc == SPK_OK) rc = enqueue_steps(fn, pp, c, exact);
     const hipError_t ee = hipStreamEndCapture(cap, &graph);
     if (rc == SPK_OK) rc = hip_check(ee, "hipStreamEndCapture");
+    // diagnostics (the memset-node evidence): SPK_GRAPH_DOT=<path> writes the captured
+    // graph's nodes and dependency edges (hipGraphDebugDotPrint) before it is instantiated
+    if (rc == SPK_OK)
+      if (const char* dot = std::getenv("SPK_GRAPH_DOT"))
+        rc = hip_check(hipGraphDebugDotPrint(graph, dot, hipGraphDebugDotFlagsVerbose), "hipGraphDebugDotPrint");
     if (rc == SPK_OK) rc = hip_check(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0), "hipGraphInstantiate");
     if (graph) (void)hipGraphDestroy(graph);
     (void)hipStreamDestroy(cap);
