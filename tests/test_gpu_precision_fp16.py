@@ -70,3 +70,31 @@ def test_fp16_mode_ragged_c3_and_eer_equality():
     # so a pair sitting at the threshold may swap order (one step = 1 / #target or #impostor)
     step = 1.0 / min(labels.sum(), (1 - labels).sum())
     assert abs(eers['fp16'] - eers['fp32']) <= step + 1e-12, eers
+
+
+# CAM++ at x1e3 (its word is set from x1e2 up): at x3e4 the scaled model itself no longer
+# holds the fp16 bar -- a CPU forward with every conv operand rounded to fp16's mantissa
+# (tools/fp16_range_probe.py measures the GPU side) reads cosine 0.767 at x1e3 and x3e4
+# against fp64, i.e. the network amplifies fp16 rounding, independent of the split's range
+@pytest.mark.parametrize('arch,key,factor', [('ecapa', 'blocks.0.norm.norm.weight', 1e5),
+                                             ('campplus', 'head.layer1.0.bn2.weight', 1e3)])
+def test_fp16_mode_scaled_split_out_of_range(arch, key, factor):
+    """The single-product kernels take the scaled split too (common.h): with activations past
+    the unscaled split's range (BN scaled as in test_gpu_range_guard.py) the fp16 mode still
+    meets its cosine bar against the fp64 forward, with the range word set and no re-run."""
+    from oracle import models_ref
+    g = helpers.golden(arch)
+    m = helpers.loaded_module(arch)
+    m.state_dict()[key].mul_(factor)
+    feats = torch.from_numpy(g['feats2'][:3])
+    sd = {k: v.double() if v.is_floating_point() else v for k, v in m.state_dict().items()}
+    ref = models_ref.forward(arch, sd, feats.double()).numpy()
+    m = m.to('cuda').set_hip_precision('fp16')
+    with torch.no_grad():
+        emb = m(feats.cuda()).cpu().numpy()
+    h = m._hip_handle(torch.device('cuda', 0))
+    assert h.last_forward_flagged and not h.last_forward_exact
+    assert np.isfinite(emb).all()
+    cos = _cos(emb.astype(np.float64), ref)
+    print(f'{arch} fp16 mode, BN x{factor:g}: min cosine {cos.min():.7f}')
+    assert cos.min() >= 0.9999, cos.min()
