@@ -217,8 +217,9 @@ def physical_cores():
 def cpu_baseline(passes, batch=64):
     """Oracle (op-for-op torch CPU restatement + numpy Fbank) on the host cores, SURVEY §8(d):
     two warm-up passes, then the best of `passes` timed passes over one batch of `batch`
-    utterances (a bounded sample of the C2 workload: a 256-utterance batch takes ~35 s per
-    pass on 16 cores, so the sample is a quarter batch; ~60 s in all)."""
+    utterances (a bounded sample of the C2 workload -- the first `batch` utterances of the
+    batch the GPU leg times: a 256-utterance batch takes ~35 s per pass on 16 cores, so the
+    sample is a quarter batch; ~60 s in all)."""
     from oracle import fbank_ref, models_ref
     from speakerlab.utils import synthetic
     from speakerlab.models.eres2net.ERes2NetV2 import ERes2NetV2
@@ -226,7 +227,9 @@ def cpu_baseline(passes, batch=64):
     torch.set_num_threads(threads)
     bn = dict(np.load(os.path.join(REPO, 'tests', 'golden', 'eres2netv2_bn.npz')))
     sd = synthetic.load_synthetic_weights(ERes2NetV2(feat_dim=80, embedding_size=192), 0, bn).state_dict()
-    wavs = synthetic.pcm16_batch(batch, SAMPLES, seed=99)
+    # the first `batch` utterances of rank 0's timed C2 batch (run(): seed 1 + 1000 rank;
+    # utterance i of a batch has its own seed, so this is a prefix of the same inputs)
+    wavs = synthetic.pcm16_batch(batch, SAMPLES, seed=1)
 
     def one(w):
         feats = torch.from_numpy(fbank_ref.fbank_batch(w, 80, mean_nor=True))
@@ -240,7 +243,7 @@ def cpu_baseline(passes, batch=64):
         one(wavs)
         best = min(best, time.perf_counter() - t0)
     return {'value': round(batch / best, 3), 'unit': 'utt/s', 'cores': threads, 'kind': 'port',
-            'sample': f'best of {passes} passes over one batch of {batch} utterances of 2 s after 2 warm-up '
+            'sample': f'best of {passes} passes over the first {batch} utterances (2 s) of the timed C2 batch after 2 warm-up '
                       f'passes over the same batch; numpy Fbank + torch CPU fp32 oracle forward, {threads} physical cores '
                       f'(lscpu, capped at the box\'s 16-CPU share); best pass {best:.2f} s'}
 
