@@ -495,7 +495,9 @@ struct Cfg {
 Cfg select_cfg(const ConvDesc& d) {
   const int M = d.nimg * d.Ho * d.Wo;
   const int bk = d.Kp >= 256 ? 32 : 16;
-  if (d.N <= 32) return {256, 32, bk, 8, 1};
+  // N <= 32 (CAM++'s CAM local convs, 128 -> 32 at M = 25,344): 256-row tiles give 99 blocks
+  // for 256 CUs; 64-row tiles (two waves) spread the same work over every CU
+  if (d.N <= 32) return (M + 255) / 256 >= 512 ? Cfg{256, 32, bk, 8, 1} : Cfg{64, 32, bk, 2, 1};
   if (d.N <= 64) return {256, 64, bk, 4, 2};
   if (M <= 4096) return {64, 128, bk, 1, 4};
   if (use_x3() && d.wh && !d.wbig) {
@@ -559,7 +561,7 @@ hipError_t launch_f32(const ConvDesc& d, hipStream_t s) {
 
 template <int BK>
 hipError_t launch_f32_bk(const ConvDesc& d, int bm, int bn, hipStream_t s) {
-  if (bn == 32) return launch_f32<256, 32, BK, 8, 1>(d, s);
+  if (bn == 32) return bm == 64 ? launch_f32<64, 32, BK, 2, 1>(d, s) : launch_f32<256, 32, BK, 8, 1>(d, s);
   if (bn == 64) return launch_f32<256, 64, BK, 4, 2>(d, s);
   if (bm == 64) return launch_f32<64, 128, BK, 1, 4>(d, s);
   if (bm == 256) return launch_f32<256, 128, BK, 4, 2>(d, s);
@@ -575,7 +577,7 @@ hipError_t launch_f32_bk(const ConvDesc& d, int bm, int bn, hipStream_t s) {
 // dispatch below and calls them.
 hipError_t conv_launch_part0(const ConvDesc& d, hipStream_t s, int bm, int bn);   // f16: 128x128
 hipError_t conv_launch_part1(const ConvDesc& d, hipStream_t s, int bm, int bn);   // f16: 256x128, 128x256
-hipError_t conv_launch_part2(const ConvDesc& d, hipStream_t s, int bm, int bn);   // f16: 256x32, 256x64, 64x128
+hipError_t conv_launch_part2(const ConvDesc& d, hipStream_t s, int bm, int bn);   // f16: 256x32, 64x32, 256x64, 64x128
 hipError_t conv_launch_part3(const ConvDesc& d, hipStream_t s, int bm, int bn, int bk);   // exact fp32, all tiles
 
 #if defined(SPK_CG_PART) && SPK_CG_PART == 0
@@ -585,8 +587,8 @@ hipError_t conv_launch_part1(const ConvDesc& d, hipStream_t s, int bm, int) {
   return bm == 256 ? launch_f16<256, 128, 4, 2>(d, s) : launch_f16<128, 256, 2, 4>(d, s);
 }
 #elif defined(SPK_CG_PART) && SPK_CG_PART == 2
-hipError_t conv_launch_part2(const ConvDesc& d, hipStream_t s, int, int bn) {
-  if (bn == 32) return launch_f16<256, 32, 8, 1>(d, s);
+hipError_t conv_launch_part2(const ConvDesc& d, hipStream_t s, int bm, int bn) {
+  if (bn == 32) return bm == 64 ? launch_f16<64, 32, 2, 1>(d, s) : launch_f16<256, 32, 8, 1>(d, s);
   if (bn == 64) return launch_f16<256, 64, 4, 2>(d, s);
   return launch_f16<64, 128, 1, 4>(d, s);
 }

@@ -154,14 +154,12 @@ __global__ void cam_context_kernel(const float* __restrict__ x, int B, int T, in
 //    (float4 column quads x row lanes, four row loads in flight, fixed-order reduction);
 //  * cam_gate: one workgroup per utterance: mean = (sum of its segment sums) / T, the
 //    contexts, and both layers with the weights staged transposed in LDS.
-__global__ void __launch_bounds__(256)
-cam_segsum_kernel(const float* __restrict__ x, int T, int C, int ld, int seg, int nseg, float* __restrict__ segsum,
-                  const int* __restrict__ vlen, const int* __restrict__ run_if) {
-  SPK_GATE(run_if);
-  __shared__ f32x4 part[256];
-  const int sg = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  const int Tb = valid_frames(vlen, b, T);
-  const int nq = C / 4, RL = blockDim.x / nq;
+// segment sg's sum of utterance b's valid rows: quad tid % nq of row lanes tid / nq, combined
+// through `part` in a fixed order; written by threads tid < nq to out[4 tid ..]
+__device__ __forceinline__ void cam_segsum_body(const float* __restrict__ x, int T, int C, int ld, int seg, int sg,
+                                                int b, int Tb, f32x4* part, float* out) {
+  const int tid = threadIdx.x;
+  const int nq = C / 4, RL = 256 / nq;
   const int cq = tid % nq, rl = tid / nq;
   const int t0 = sg * seg, t1 = min(Tb, t0 + seg);
   f32x4 a = {0.f, 0.f, 0.f, 0.f};
@@ -182,8 +180,17 @@ cam_segsum_kernel(const float* __restrict__ x, int T, int C, int ld, int seg, in
   if (tid < nq) {
     f32x4 v = part[tid];
     for (int r = 1; r < RL; ++r) v += part[r * nq + tid];
-    *reinterpret_cast<f32x4*>(segsum + ((size_t)b * nseg + sg) * C + tid * 4) = v;
+    *reinterpret_cast<f32x4*>(out + tid * 4) = v;
   }
+}
+
+__global__ void __launch_bounds__(256)
+cam_segsum_kernel(const float* __restrict__ x, int T, int C, int ld, int seg, int nseg, float* __restrict__ segsum,
+                  const int* __restrict__ vlen, const int* __restrict__ run_if) {
+  SPK_GATE(run_if);
+  __shared__ f32x4 part[256];
+  const int sg = blockIdx.x, b = blockIdx.y;
+  cam_segsum_body(x, T, C, ld, seg, sg, b, valid_frames(vlen, b, T), part, segsum + ((size_t)b * nseg + sg) * C);
 }
 
 __global__ void __launch_bounds__(1024)
@@ -266,19 +273,16 @@ cam_gate_kernel(const float* __restrict__ segsum, int T, int C, int seg, int nse
 // transposed into LDS per block, partial dots over Q = 256 / N contiguous K-slices combined by
 // a butterfly over the Q neighbouring lanes (fixed order).  Requires 256 % red == 0,
 // 256 % growth == 0, C % (4 * (256 / red)) == 0, red % (4 * (256 / growth)) == 0 (host).
-__global__ void __launch_bounds__(256)
-cam_gate_lean_kernel(const float* __restrict__ segsum, int T, int C, int seg, int nseg, const float* __restrict__ w1,
-                     int k1p, const float* __restrict__ b1, int red, const float* __restrict__ w2, int k2p,
-                     const float* __restrict__ b2, int growth, float* __restrict__ gate, int ldg,
-                     const int* __restrict__ vlen, const int* __restrict__ run_if) {
-  SPK_GATE(run_if);
-  extern __shared__ float sm[];
+// `ss`: utterance b's segment sums [nseg][C] (global memory, or LDS in the fused kernel);
+// `sm`: C + CAM_SEGS (C + red) floats of LDS
+__device__ __forceinline__ void cam_gate_lean_body(const float* ss, int C, int seg, int nseg, const float* __restrict__ w1,
+                                                   int k1p, const float* __restrict__ b1, int red,
+                                                   const float* __restrict__ w2, int k2p, const float* __restrict__ b2,
+                                                   int growth, float* __restrict__ gate, int ldg, int b, int Tb, float* sm) {
   float* mean = sm;                         // [C]
   float* ctx = mean + C;                    // [CAM_SEGS][C]
   float* h = ctx + CAM_SEGS * C;            // [CAM_SEGS][red]
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const int Tb = valid_frames(vlen, b, T);
-  const float* ss = segsum + (size_t)b * nseg * C;
+  const int tid = threadIdx.x;
   // this thread's weight slices and biases of both layers, requested first: the phases below
   // are a chain of dependent steps, and a weight load at its use was one more L2 round trip
   // in it (host: K / Q <= 4 * CAM_WQ for both layers)
@@ -344,6 +348,39 @@ cam_gate_lean_kernel(const float* __restrict__ segsum, int T, int C, int seg, in
     __syncthreads();
     dense(h, red, wq2, bq2, growth, false, ns, gate + ((size_t)b * nseg + s0) * ldg, ldg);
   }
+}
+
+__global__ void __launch_bounds__(256)
+cam_gate_lean_kernel(const float* __restrict__ segsum, int T, int C, int seg, int nseg, const float* __restrict__ w1,
+                     int k1p, const float* __restrict__ b1, int red, const float* __restrict__ w2, int k2p,
+                     const float* __restrict__ b2, int growth, float* __restrict__ gate, int ldg,
+                     const int* __restrict__ vlen, const int* __restrict__ run_if) {
+  SPK_GATE(run_if);
+  extern __shared__ float sm[];
+  const int b = blockIdx.x;
+  cam_gate_lean_body(segsum + (size_t)b * nseg * C, C, seg, nseg, w1, k1p, b1, red, w2, k2p, b2, growth, gate, ldg, b,
+                     valid_frames(vlen, b, T), sm);
+}
+
+// The segment sums and the lean gate in one launch (one workgroup per utterance; the sums stay
+// in LDS): CAM++ runs this pair once per dense layer, 52 times a forward, and the two launches
+// of ~7 us each were dominated by their fixed cost.  Same arithmetic and order as the pair.
+__global__ void __launch_bounds__(256)
+cam_gate_fused_kernel(const float* __restrict__ x, int T, int C, int ld, int seg, int nseg, const float* __restrict__ w1,
+                      int k1p, const float* __restrict__ b1, int red, const float* __restrict__ w2, int k2p,
+                      const float* __restrict__ b2, int growth, float* __restrict__ gate, int ldg,
+                      const int* __restrict__ vlen, const int* __restrict__ run_if) {
+  SPK_GATE(run_if);
+  extern __shared__ float sm[];
+  f32x4* part = reinterpret_cast<f32x4*>(sm);            // [256] segment-sum partials
+  float* ssl = sm + 4 * 256;                             // [nseg][C]
+  const int b = blockIdx.x;
+  const int Tb = valid_frames(vlen, b, T);
+  for (int sg = 0; sg < nseg; ++sg) {
+    cam_segsum_body(x, T, C, ld, seg, sg, b, Tb, part, ssl + (size_t)sg * C);
+    __syncthreads();                                     // sums written, partials free again
+  }
+  cam_gate_lean_body(ssl, C, seg, nseg, w1, k1p, b1, red, w2, k2p, b2, growth, gate, ldg, b, Tb, ssl + (size_t)nseg * C);
 }
 
 __global__ void stats_pool_kernel(const float* __restrict__ x, int B, int T, int C, int ld, float* __restrict__ out,
@@ -415,15 +452,22 @@ hipError_t launch_cam_gate(const float* x, int B, int T, int C, int ld, int seg,
                           int ldg, float* segsum, hipStream_t s, const int* vlen) {
   if (C % 4 || C / 4 > 256 || ld % 4 || red <= 0 || red > 1024 || growth <= 0 || growth > 1024 || B <= 0 || nseg <= 0)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(cam_segsum_kernel, dim3(nseg, B), dim3(256), 0, s, x, T, C, ld, seg, nseg, segsum, vlen, launch_gate());
-  if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   static const bool lean_off = std::getenv("SPK_CAM_GATE_LDS") != nullptr;   // A/B: the transposing kernel
+  static const bool fuse_off = std::getenv("SPK_CAM_GATE_PAIR") != nullptr;  // A/B: segment sums as their own launch
   // the lean kernel's butterfly sums Q = 256 / red (or 256 / growth) adjacent lanes with
   // __shfl_xor, i.e. within one wave only when Q <= 64
   const bool lean = !lean_off && red >= 4 && growth >= 4 && 256 % red == 0 && 256 % growth == 0 && C % (4 * (256 / red)) == 0 &&
                     red % (4 * (256 / growth)) == 0 && C / (256 / red) <= 4 * CAM_WQ &&
                     red / (256 / growth) <= 4 * CAM_WQ && k1p % 4 == 0 && k2p % 4 == 0 &&
                     (reinterpret_cast<uintptr_t>(w1) & 15) == 0 && (reinterpret_cast<uintptr_t>(w2) & 15) == 0;
+  const size_t lds_f = sizeof(float) * (4 * 256 + (size_t)nseg * C + C + CAM_SEGS * ((size_t)C + red));
+  if (lean && !fuse_off && lds_f <= 64 * 1024) {
+    hipLaunchKernelGGL(cam_gate_fused_kernel, dim3(B), dim3(256), lds_f, s, x, T, C, ld, seg, nseg, w1, k1p, b1, red,
+                       w2, k2p, b2, growth, gate, ldg, vlen, launch_gate());
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(cam_segsum_kernel, dim3(nseg, B), dim3(256), 0, s, x, T, C, ld, seg, nseg, segsum, vlen, launch_gate());
+  if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   if (lean) {
     const size_t lds_l = sizeof(float) * ((size_t)C + CAM_SEGS * ((size_t)C + red));
     hipLaunchKernelGGL(cam_gate_lean_kernel, dim3(B), dim3(256), lds_l, s, segsum, T, C, seg, nseg, w1, k1p, b1, red,
