@@ -250,10 +250,8 @@ void build_campplus(Builder& b, int T) {
         ConvDesc d;
         d.nimg = B; d.Ho = 1; d.Wo = T2;
         d.s0 = src2d(db, cin, 1, 1, 1, 1, 0, 0);
-        d.s0.pre_scale = m.dptr(pre->ps_off);
-        d.s0.pre_shift = m.dptr(pre->pt_off);
         d.ldo = bnc; d.act = ACT_RELU;
-        Builder::ConvIO io; io.s0 = bk.buf; io.out = Hh; io.vlen = LEN2; io.rowlen = LEN2;
+        Builder::ConvIO io; io.s0 = bk.buf; io.out = Hh; io.vlen = LEN2; io.rowlen = LEN2; io.pre = pre;
         b.macs_per_utt += m_l1;
         b.conv(q + ".linear1", d, l1, io);
       }
@@ -310,11 +308,9 @@ void build_campplus(Builder& b, int T) {
       ConvDesc d;
       d.nimg = B; d.Ho = 1; d.Wo = T2;
       d.s0 = src2d(db, bk.c_fin, 1, 1, 1, 1, 0, 0);
-      d.s0.pre_scale = m.dptr(pre->ps_off);
-      d.s0.pre_shift = m.dptr(pre->pt_off);
       d.ldo = ldd;
       if (last) d.act = ACT_RELU;
-      Builder::ConvIO io; io.s0 = bk.buf; io.out = dst; io.vlen = LEN2; io.rowlen = LEN2;
+      Builder::ConvIO io; io.s0 = bk.buf; io.out = dst; io.vlen = LEN2; io.rowlen = LEN2; io.pre = pre;
       b.conv(t, d, tp, io, /*use_bias=*/last);
     }
   }

@@ -80,6 +80,10 @@ struct ConvDesc {
   // null: that kernel is not used)
   const uint16_t* wf = nullptr;
   const int* range_in = nullptr;  // scaled split (below): the forward's range word, read for the operand scale
+  // extra operand scale bits for a GEMM whose loader amplifies its operand (CAM++'s BN-ReLU
+  // pre-activation, s0.pre_scale): relu(psc x + psh) can exceed the 2x growth bound the word
+  // assumes, so the operand is scaled by a further 2^-range_bits (Builder::conv, pre_range_bits)
+  int range_bits = 0;
 };
 
 // fp16x3 range guard.  The split-precision GEMMs represent an operand as two fp16 values,
@@ -101,7 +105,12 @@ struct ConvDesc {
 //    word * 2^-s < kRangeLimit, and its accumulator by 2^s (both exact: powers of two).  Every
 //    operand is at most twice the largest value any earlier producer wrote, which the word
 //    holds by the time the GEMM starts, so the scaled operand stays below 2^15; relative
-//    precision is that of the unscaled split.  A block may read a larger word than another
+//    precision is that of the unscaled split.
+//    A loader that applies an affine pre-activation (CAM++ BN-ReLU, |relu(psc x + psh)| <=
+//    |psc| |x| + |psh|) breaks the 2x growth bound by up to P = max_c max(|psc|, |psh| / 2^14):
+//    with |x| < 2 max(word, 2^14) the operand is below 1.5 P 2^(e+2) (e: the word's exponent,
+//    13 when clear), so a further 2^-b with P <= 1.3 * 2^b keeps the scaled operand below
+//    2^15 again (host: pre_range_bits, ConvDesc::range_bits; applied in the twin plans too).  A block may read a larger word than another
 //    (producers of its own launch raising it meanwhile): each block undoes its own scale, so
 //    every output is consistent.
 constexpr float kRangeLimit = 16384.0f;
@@ -112,13 +121,15 @@ __device__ __forceinline__ void range_note(int* flag, float amax) {
   if (flag && amax >= kRangeLimit) atomicMax(flag, __float_as_int(amax));
 }
 // operand scale of a scaled-split GEMM (above): 1 while the word is clear (or absent, or
-// non-finite: the result is inf / NaN either way), else 2^-s with word * 2^-s in [2^13, 2^14)
-__device__ __forceinline__ float range_scale(const int* word) {
-  if (!word) return 1.f;
-  const int w = *word;
-  if (w < 0x46800000 || w >= 0x7F800000) return 1.f;       // below 2^14 (i.e. 0), or inf / NaN
-  const int e = (w >> 23) - 127;                             // word in [2^e, 2^(e+1)), e >= 14
-  return __int_as_float((127 - (e - 13)) << 23);             // 2^-(e-13)
+// non-finite: the result is inf / NaN either way), else 2^-s with word * 2^-s in [2^13, 2^14);
+// times 2^-bits for an amplifying operand loader (ConvDesc::range_bits)
+__device__ __forceinline__ float range_scale(const int* word, int bits = 0) {
+  int s = 0;
+  if (word) {
+    const int w = *word;
+    if (w >= 0x46800000 && w < 0x7F800000) s = ((w >> 23) - 127) - 13;   // word in [2^e, 2^(e+1)), e >= 14
+  }
+  return __int_as_float((127 - min(s + bits, 126)) << 23);   // 2^-(s + bits), kept normal
 }
 // 2^k * sc and 2^k / sc of a power-of-two scale by exponent arithmetic (scalar integer ops:
 // the values stay in SGPRs instead of taking a VGPR each for a float multiply / divide)
@@ -228,6 +239,8 @@ hipError_t launch_gemm_f(const ConvDesc& d, hipStream_t s);
 std::string gemm_f_kernel_name(const ConvDesc& d);
 size_t frag_halves(int N, int Kp);   // size of one matrix in fragment order (N padded to 128)
 hipError_t launch_pack_frag(const uint16_t* wh, const uint16_t* wl, int N, int Kp, uint16_t* out, hipStream_t s);
+
+int device_cus();   // CU count of the current device, cached per device (pw_gemm.hip)
 
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 

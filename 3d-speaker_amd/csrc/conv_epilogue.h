@@ -168,11 +168,21 @@ __device__ __forceinline__ float epilogue_elem(const ConvDesc& d, int m, int n, 
 struct NoHook {
   __device__ void operator()() const {}
 };
-template <int TM, int TN, bool LEAN = false, bool PLAIN = false, bool WIDE = false, class RowMap, class Hook = NoHook>
+// L16 = true: each 32x32 tile holds four 16x16x32-MFMA accumulators (quadrant q = 2 a + b at
+// elements 4 q .. 4 q + 3: row 16 a + 4 (lane >> 4) + e, column 16 b + (lane & 15)); the slab
+// rows are then padded to 36 floats (the four lane groups of a store land 144 floats apart:
+// distinct banks, where 128 apart would be a 4-way conflict).  epi_slab_floats() sizes it.
+template <bool L16>
+__host__ __device__ constexpr int epi_srow() { return L16 ? 36 : 32; }
+template <bool L16>
+__host__ __device__ constexpr int epi_slab_floats() { return 32 * epi_srow<L16>(); }
+template <int TM, int TN, bool LEAN = false, bool PLAIN = false, bool WIDE = false, bool L16 = false, class RowMap,
+          class Hook = NoHook>
 __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f32x16 (&acc)[TM][TN], int wave,
                                                int lane, int nwave, int M, RowMap rowmap,
                                                const f32x4* pre_bias = nullptr, Hook hook = Hook{}) {
   const int li = lane & 31, lh = lane >> 5;
+  constexpr int SROW = epi_srow<L16>(), SLAB = epi_slab_floats<L16>();
   // one 32x32 accumulator tile at a time through a per-wave LDS slab:
   // registers -> LDS in the MFMA C layout (col = lane&31, row = (r&3)+8(r>>2)+4(lane>>5)),
   // then each lane owns 4 consecutive columns of 4 rows (8 lanes = one 128-B output row):
@@ -180,13 +190,19 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
   // tile's loads are issued before the first use, so the fused epilogue costs one memory
   // round trip per tile instead of sixteen dependent scalar ones.
   // all of the wave's accumulators go to LDS first, so they are dead during the epilogue
-  float* cw = lds + wave * (TM * TN * 1024);
+  float* cw = lds + wave * (TM * TN * SLAB);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) cw[(i * TN + j) * 1024 + ((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[i][j][r];
+      for (int r = 0; r < 16; ++r) {
+        if constexpr (L16)
+          cw[(i * TN + j) * SLAB + (16 * (r >> 3) + 4 * (lane >> 4) + (r & 3)) * SROW + 16 * ((r >> 2) & 1) + (lane & 15)] =
+              acc[i][j][r];
+        else
+          cw[(i * TN + j) * SLAB + ((r & 3) + 8 * (r >> 2) + 4 * lh) * SROW + li] = acc[i][j][r];
+      }
   wave_lds_sync();
   float* part = d.ksplit > 1 ? d.partial + (size_t)blockIdx.z * M * d.N : nullptr;
   const bool vec = (d.N % 4 == 0) && (d.ldo % 4 == 0) && (!d.res || d.ldr % 4 == 0) &&
@@ -237,7 +253,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
           // before it, i.e. the next tile's prefetch); all four rows are computed first and
           // stored back to back from distinct registers.
           const f32x4 bias = pre_bias[tile];
-          const float* ct = cw + tile * 1024;
+          const float* ct = cw + tile * SLAB;
           float* const ocol = d.out + n;
           f32x4 o[4];
           int mq[4];
@@ -248,7 +264,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
             for (int q = 0; q < 4; ++q) {
               const int rl = q * 8 + (lane >> 3);
               mq[q] = rowmap(i * 32 + rl);
-              o[q] = *reinterpret_cast<const f32x4*>(ct + rl * 32 + c4) + bias;
+              o[q] = *reinterpret_cast<const f32x4*>(ct + rl * SROW + c4) + bias;
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 if constexpr (A >= 0) o[q][e] = apply_act(o[q][e], A);
@@ -272,7 +288,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
         if (n >= d.N) continue;
         float* const ocol = out_at(d, 0, n);   // plane / column split once per tile, not per row
         const f32x4 bias = bias4[tile], ps = ps4[tile], pt = pt4[tile];
-        const float* ct = cw + tile * 1024;
+        const float* ct = cw + tile * SLAB;
         // the rows of a tile with the layer's activation resolved once (not per element): the
         // common forms (one activation, no post-affine, no ragged mask) as compile-time
         // variants, everything else through the general form
@@ -283,7 +299,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
             const int rl = q * 8 + (lane >> 3);
             const int m = rowmap(i * 32 + rl);
             if (m < 0 || m >= M) continue;
-            f32x4 o = *reinterpret_cast<const f32x4*>(ct + rl * 32 + c4) + bias + ra4[tile][q];
+            f32x4 o = *reinterpret_cast<const f32x4*>(ct + rl * SROW + c4) + bias + ra4[tile][q];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               if constexpr (A >= 0) {
@@ -339,7 +355,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
         float* const ocol = out_at(d, 0, n);
         f32x4 bias = {0.f, 0.f, 0.f, 0.f};
         if (d.bias) bias = *reinterpret_cast<const f32x4*>(d.bias + n);
-        const float* ct = cw + tile * 1024;
+        const float* ct = cw + tile * SLAB;
         if constexpr (PLAIN) {
           // all four rows computed first, then four back-to-back stores from distinct
           // registers: a store whose source registers are reused right away makes the
@@ -350,7 +366,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
           for (int q = 0; q < 4; ++q) {
             const int rl = q * 8 + (lane >> 3);
             mq[q] = rowmap(i * 32 + rl);
-            o[q] = *reinterpret_cast<const f32x4*>(ct + rl * 32 + c4) + bias;
+            o[q] = *reinterpret_cast<const f32x4*>(ct + rl * SROW + c4) + bias;
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[q][e] = apply_act(apply_act(o[q][e], d.act), d.act2);
             amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[q][0]), fabsf(o[q][1])), fmaxf(fabsf(o[q][2]), fabsf(o[q][3]))));
@@ -365,7 +381,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
           const int rl = q * 8 + (lane >> 3);
           const int m = rowmap(i * 32 + rl);
           if (m < 0 || m >= M) continue;
-          f32x4 o = *reinterpret_cast<const f32x4*>(ct + rl * 32 + c4) + bias;
+          f32x4 o = *reinterpret_cast<const f32x4*>(ct + rl * SROW + c4) + bias;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             o[e] = aff_combine(o[e], xa[tile][q][e], ya[tile][q][e]);
@@ -387,7 +403,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
   for (int tile = 0; tile < TM * TN; ++tile) {
     {
       const int i = tile / TN, j = tile % TN;
-      const float* ct = cw + tile * 1024;
+      const float* ct = cw + tile * SLAB;
       const int nbase = nwave + j * 32;
       if (vec) {
         const int c4 = (lane & 7) * 4;
@@ -408,7 +424,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             const int rl = (half * 2 + q) * 8 + (lane >> 3);
-            v[q] = *reinterpret_cast<const f32x4*>(ct + rl * 32 + c4);
+            v[q] = *reinterpret_cast<const f32x4*>(ct + rl * SROW + c4);
             if (!part && n < d.N) {
               const int m = max(0, min(rowmap(i * 32 + rl), M - 1));
               if (d.res) ra4[q] = *reinterpret_cast<const f32x4*>(d.res + (size_t)m * d.ldr + n);
@@ -460,7 +476,7 @@ __device__ __forceinline__ void epilogue_tiles(const ConvDesc& d, float* lds, f3
           const int rl = 2 * q + lh;
           const int m = rowmap(i * 32 + rl);
           if (m >= 0 && m < M && n < d.N) {
-            const float v = ct[rl * 32 + li];
+            const float v = ct[rl * SROW + li];
             if (part) {
               part[(size_t)m * d.N + n] = v;
             } else {

@@ -414,7 +414,7 @@ template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE, bool BUF,
 __device__ __forceinline__ void conv_gemm_f16_entry(const ConvDesc& d) {
   SPK_GATE(d.run_if);
   __shared__ __attribute__((aligned(16))) float lds[X3Cfg<BM, BN, WM, WN, X1>::LDS_FLOATS];
-  const float sc = range_scale(d.range_in);
+  const float sc = range_scale(d.range_in, d.range_bits);
   if (sc == 1.0f) conv_gemm_f16_body<BM, BN, WM, WN, S1, ADD, PRE, BUF, X1, false>(d, lds, 1.0f);
   else conv_gemm_f16_body<BM, BN, WM, WN, S1, ADD, PRE, BUF, X1, true>(d, lds, sc);
 }

@@ -39,6 +39,9 @@
                         // (mixed, off), 4 the two-set loop splits between its k-steps too (0-3 %
                         // on the 128 x 128 layers)
 #endif
+#ifndef SPK_F_M16
+#define SPK_F_M16 0   // 1: v_mfma_f32_16x16x32_f16 (fragments packed for it, epilogue_tiles L16 layout)
+#endif
 #ifndef SPK_FEXP
 #define SPK_FEXP 0   // ablation builds only (tools/fexp.sh), bit mask: 1 no MFMA, 2 no in-loop A loads,
                      // 4 no in-loop A split / stores, 8 no in-loop B DMA, 16 no epilogue stores
@@ -68,9 +71,10 @@ struct FCfg {
   static constexpr int STAGE = ASTAGE + CHUNKS * 1024;
   // epilogue_tiles' slab: the whole wave tile when it fits next to nothing else (128 x 128),
   // else one row of accumulator tiles at a time
-  static constexpr int EPI_ALL = WM * WN * TM * TN * 1024 * 4;
+  static constexpr int SLAB = epi_slab_floats<SPK_F_M16 != 0>() * 4;   // bytes per 32x32 tile
+  static constexpr int EPI_ALL = WM * WN * TM * TN * SLAB;
   static constexpr bool EPI_ONE = EPI_ALL <= 2 * STAGE;
-  static constexpr int EPI = EPI_ONE ? EPI_ALL : WM * WN * TN * 1024 * 4;
+  static constexpr int EPI = EPI_ONE ? EPI_ALL : WM * WN * TN * SLAB;
   static constexpr int LDS = 2 * STAGE > EPI ? 2 * STAGE : EPI;
   static constexpr int ROWS = BM / (NT / 8);         // A rows staged per thread
   static constexpr bool ONE_SET = TM * TN >= 8;     // 128 accumulator registers per wave
@@ -118,7 +122,7 @@ template <int BM, int BN, int WM, int WN, int OP2>
 __global__ void __launch_bounds__(64 * WM * WN, (FCfg<BM, BN, WM, WN>::WAVES_PER_EU))
 conv_gemm_x3f_kernel(const ConvDesc d) {
   SPK_GATE(d.run_if);
-  const float sc = range_scale(d.range_in);            // scaled split: operand x 2^-s (common.h)
+  const float sc = range_scale(d.range_in, d.range_bits);            // scaled split: operand x 2^-s (common.h)
   using C = FCfg<BM, BN, WM, WN>;
   constexpr bool ADD = OP2 == 1, S1 = OP2 == 2;
   constexpr int TM = C::TM, TN = C::TN, ROWS = C::ROWS, NT = C::NT;
@@ -262,6 +266,48 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
     }
   };
 
+#if SPK_F_M16
+  // 16x16x32 form: each 32x32 tile of the wave is four 16x16 accumulators; a K-tile is one
+  // MFMA k-step (K = 32).  compute_s(buf, s) runs row half s (16-row blocks s*TM .. s*TM+TM-1)
+  // of the wave tile; half 0 also reads the B fragments (kept in registers for half 1).
+  // Fragment order (pack_frag_kernel M16): chunk (32-col tile j, 16-col half h, plane p) at
+  // j * 4096 + (2 h + p) * 1024, lane l: column 16 h + (l & 15), k = 8 (l >> 4) + e.
+  f32x4 acc[2 * TM][2 * TN];
+#pragma unroll
+  for (int i = 0; i < 2 * TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2 * TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f16x8 bh[2 * TN], bl[2 * TN], bh2[2 * TN];
+  auto compute_s = [&](int buf, int s) {
+    const _Float16* ahi = reinterpret_cast<const _Float16*>(lb + buf * C::STAGE);
+    if (s == 0) {
+      const char* bb = lb + buf * C::STAGE + C::ASTAGE + wn * TN * 4096 + lane * 16;
+#pragma unroll
+      for (int j = 0; j < 2 * TN; ++j) {
+        bh[j] = *reinterpret_cast<const f16x8*>(bb + (j >> 1) * 4096 + (j & 1) * 2048);
+        bl[j] = *reinterpret_cast<const f16x8*>(bb + (j >> 1) * 4096 + (j & 1) * 2048 + 1024);
+        bh2[j] = bh[j] * (_Float16)2048.0f;   // exact (|w| < 31.5: ConvDesc::wbig)
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < TM; ++ii) {
+      const int i = s * TM + ii;
+      const _Float16* p = ahi + (wm * TM * 32 + i * 16 + (lane & 15)) * C::LROW + 8 * (lane >> 4);
+      const f16x8 ah = *reinterpret_cast<const f16x8*>(p);
+      const f16x8 al = *reinterpret_cast<const f16x8*>(p + C::PA);
+#pragma unroll
+      for (int j = 0; j < 2 * TN; ++j) {
+        if (SPK_FEXP & 1) {
+          acc[i][j][0] += (float)ah[0] + (float)bh2[j][1] + (float)bl[j][2] + (float)al[3] + (float)bh[j][4];
+          continue;
+        }
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh2[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+#else
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -303,6 +349,7 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
         }
     }
   };
+#endif
   auto compute = [&](int buf) {
     compute_s(buf, 0);
     compute_s(buf, 1);
@@ -408,17 +455,41 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
   }
   });
   const float back = pow2_div(sc, -11);               // 2^(-11) / sc, exact
+#if SPK_F_M16
+  // the four 16x16 accumulators of 32x32 tile (i, j) as one f32x16 (epilogue_tiles L16)
+  auto tile = [&](int i, int j) {
+    f32x16 t;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[4 * q + e] = acc[2 * i + (q >> 1)][2 * j + (q & 1)][e] * back;
+    return t;
+  };
+  constexpr bool L16 = true;
+#else
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] *= back;
+  auto tile = [&](int i, int j) { return acc[i][j]; };
+  constexpr bool L16 = false;
+#endif
 #if SPK_FEXP & 16
-  if (acc[0][0][0] == 1234.5f && acc[TM - 1][TN - 1][3] == 77.f) d.out[tid] = acc[0][0][1];
+  {
+    const f32x16 t0 = tile(0, 0), t1 = tile(TM - 1, TN - 1);
+    if (t0[0] == 1234.5f && t1[3] == 77.f) d.out[tid] = t0[1];
+  }
 #else
   // one row of accumulator tiles at a time through the wave's slab (TN x 4 KB): the whole
   // wave tile of a 256-wide block would not fit in LDS
   if constexpr (C::EPI_ONE) {
-    epilogue_tiles<TM, TN>(d, lds, acc, wave, lane, n0 + wn * TN * 32, M, [&](int r) { return m0 + wm * TM * 32 + r; });
+    f32x16 all[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) all[i][j] = tile(i, j);
+    epilogue_tiles<TM, TN, false, false, false, L16>(d, lds, all, wave, lane, n0 + wn * TN * 32, M,
+                                                     [&](int r) { return m0 + wm * TM * 32 + r; });
     return;
   }
   // compile-time row index (a runtime one, e.g. from a loop the compiler does not unroll around
@@ -428,8 +499,9 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
     const int rb = m0 + wm * TM * 32 + i * 32;
     f32x16 row[1][TN];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) row[0][j] = acc[i][j];
-    epilogue_tiles<1, TN>(d, lds, row, wave, lane, n0 + wn * TN * 32, M, [&](int r) { return rb + r; });
+    for (int j = 0; j < TN; ++j) row[0][j] = tile(i, j);
+    epilogue_tiles<1, TN, false, false, false, L16>(d, lds, row, wave, lane, n0 + wn * TN * 32, M,
+                                                    [&](int r) { return rb + r; });
   };
   StaticFor<0, TM>::run(epi_row);
 #endif
@@ -447,7 +519,12 @@ __global__ void pack_frag_kernel(const uint16_t* __restrict__ wh, const uint16_t
     const int p = (int)(ch & 1), s = (int)((ch >> 1) & 1);
     const size_t kj = ch >> 2;
     const int j = (int)(kj % NJ), kt = (int)(kj / NJ);
+#if SPK_F_M16
+    // (s = the 16-column half) n = 32 j + 16 s + (lane & 15), k = 32 kt + 8 (lane >> 4) + e
+    const int n = 32 * j + 16 * s + (lane & 15), k = 32 * kt + 8 * (lane >> 4);
+#else
     const int n = 32 * j + (lane & 31), k = 32 * kt + 16 * (lane >> 5) + 8 * s;
+#endif
     u32x4 v = {0u, 0u, 0u, 0u};
     if (n < N) v = *reinterpret_cast<const u32x4*>((p ? wl : wh) + (size_t)n * Kp + k);
     *reinterpret_cast<u32x4*>(out + i * 8) = v;
@@ -504,12 +581,7 @@ FTile f_tile(const ConvDesc& d) {
   // conv3s of layer 3, K = 208, gain: 425 -> 396 us).
   const int M = d.nimg * d.Ho * d.Wo;
   if (d.N > 128 && M >= 16384 && !has_add(d) && !has_s1(d) && (d.Kp >= 512 || (!d.affx && !d.gate))) {
-    static int cus = 0;
-    if (!cus) {
-      int dev = 0, n = 0;
-      cus = (hipGetDevice(&dev) == hipSuccess &&
-             hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0) ? n : 256;
-    }
+    const int cus = device_cus();
     const double rounds = (double)((M + 255) / 256) * ((d.N + 255) / 256) / cus;
     const double tail = rounds - (int)rounds;
     if (rounds >= 4.0 || tail == 0.0 || tail >= 0.6) return {256, 256};

@@ -20,6 +20,8 @@
 #include <string>
 #include <type_traits>
 
+#include <atomic>
+
 #include "common.h"
 #include "conv_epilogue.h"
 
@@ -51,7 +53,7 @@ __global__ void __launch_bounds__(512, 1)
 pw_gemm_x3_kernel(const ConvDesc d) {
   SPK_GATE(d.run_if);
   // scaled split (common.h): operand x 2^-s at staging, accumulators x 2^s in the epilogue
-  const float sc = range_scale(d.range_in), back = pow2_div(sc, 0), back_x = pow2_div(sc, -11);
+  const float sc = range_scale(d.range_in, d.range_bits), back = pow2_div(sc, 0), back_x = pow2_div(sc, -11);
   using C = PwCfg<KP, BN>;
   __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
   _Float16* Bh = reinterpret_cast<_Float16*>(lds);
@@ -221,18 +223,6 @@ pw_gemm_x3_kernel(const ConvDesc d) {
   }
 }
 
-int device_cus_pw() {
-  static int cached[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (!cached[dev]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cached[dev] = n;
-  }
-  return cached[dev];
-}
-
 template <int KP, int BN, bool S1, bool RES>
 hipError_t launch_pw_t(const ConvDesc& d, hipStream_t s) {
   using C = PwCfg<KP, BN>;
@@ -246,7 +236,7 @@ hipError_t launch_pw_t(const ConvDesc& d, hipStream_t s) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 512, 0) != hipSuccess || n <= 0) n = 1;
     return n;
   }();
-  const int slots = per_cu * device_cus_pw();
+  const int slots = per_cu * device_cus();
   const int grid = std::max(nN, std::min(mtiles * nN, slots / nN * nN));
   hipLaunchKernelGGL(k, dim3(grid), dim3(512), 0, s, d);
   return hipGetLastError();
@@ -257,6 +247,20 @@ hipError_t launch_pw_t(const ConvDesc& d, hipStream_t s) {
 int pw_bn(const ConvDesc& d) { return d.Kp == 32 ? 32 : d.N <= 64 ? 64 : 128; }
 
 }  // namespace
+
+int device_cus() {
+  // per device (handles on different GPU models in one process), relaxed atomics: a racing
+  // first query stores the same value twice
+  static std::atomic<int> cached[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  int n = cached[dev].load(std::memory_order_relaxed);
+  if (!n) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev].store(n, std::memory_order_relaxed);
+  }
+  return n;
+}
 
 bool pw_supported(const ConvDesc& d) {
   static const bool off = std::getenv("SPK_NO_PW") != nullptr;   // diagnostics: implicit GEMM instead

@@ -487,13 +487,6 @@ res2_block_kernel(const Res2Desc d) {
 #endif
 }
 
-int device_cus_r2() {
-  int dev = 0, n = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 256;
-  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 256;
-  return n;
-}
-
 }  // namespace
 
 bool res2_block_supported(const Res2Desc& d) {
@@ -511,7 +504,7 @@ std::string res2_block_kernel_name(const Res2Desc& d) {
 hipError_t launch_res2_block(const Res2Desc& d, hipStream_t s) {
   if (!res2_block_supported(d) || d.x == d.out) return hipErrorInvalidValue;
   const int ntiles = d.nimg * ((d.W + 15) / 16) * ((d.H + 7) / 8);
-  int grid = std::min(device_cus_r2(), (ntiles + 7) / 8 * 8);
+  int grid = std::min(device_cus(), (ntiles + 7) / 8 * 8);
   grid = std::max(8, grid / 8 * 8);
   if (d.proj) hipLaunchKernelGGL((res2_block_kernel<64, 128, true>), dim3(grid), dim3(512), 0, s, d);
   else hipLaunchKernelGGL((res2_block_kernel<128, 128, false>), dim3(grid), dim3(512), 0, s, d);

@@ -206,8 +206,23 @@ void Builder::step(const std::string& name, Step s, const std::string& kernel, d
   macs_at_last_step = macs_per_utt;
 }
 
+int pre_range_bits(const Packed& pre) {
+  const double P = std::max(pre.l1max, pre.bmax / kRangeLimit);
+  int b = 0;
+  while (b < 126 && P > 1.3 * std::ldexp(1.0, b)) ++b;
+  return b;
+}
+
 void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const ConvIO& io, bool use_bias) {
   if (!plan) return;
+  if (io.pre) {
+    d.s0.pre_scale = m.dptr(io.pre->ps_off);
+    d.s0.pre_shift = m.dptr(io.pre->pt_off);
+    d.range_bits = pre_range_bits(*io.pre);
+  } else if (d.s0.pre_scale) {
+    // the operand bound of the scaled split needs the pre-activation's host-side extremes
+    throw SpkError(SPK_E_INVALID, "internal: pre-activation without its packed affine: " + name);
+  }
   d.N = p.N; d.K = p.K; d.Kp = p.Kp;
   d.kcb = p.kcb;
   if (p.kcb && (d.s0.kh * d.s0.kw * d.s0.cin != d.K || d.s0.cin % 32 || io.s1))

@@ -195,9 +195,14 @@ struct Builder {
   struct ConvIO {
     Buf s0, s0b, s1, out, res, affx, affy, gate, partial, rowbias;
     Buf rowlen, vlen;   // ragged batches (int32 arrays): output / s0-input valid time extents
+    const Packed* pre = nullptr;   // s0's BN-ReLU pre-activation (Model::pack_post_affine)
   };
   void conv(const std::string& name, ConvDesc d, const Packed& p, const ConvIO& io, bool use_bias = true);
 };
+
+// operand scale bits for a GEMM whose loader applies the pre-activation `pre` (common.h
+// ConvDesc::range_bits): the smallest b >= 0 with max_c max(|psc|, |psh| / 2^14) <= 1.3 * 2^b
+int pre_range_bits(const Packed& pre);
 
 void build_eres2net(Builder& b, int T, bool v2);
 void build_ecapa(Builder& b, int T);

@@ -35,8 +35,8 @@ def test_golden_embeddings(arch):
         e64 = helpers.rel_err(emb, g[f'emb64_{i}']).max()
         e32 = helpers.rel_err(emb, g[f'emb32_{i}']).max()
         # variants with a reference fp32-vs-fp64 floor above the bar (w24s4ep4: 5e-4 with
-        # random weights) are held to 2x that floor; the four north-star models to 1e-4
-        tol = max(TOL, 2 * helpers.rel_err(g[f'emb32_{i}'], g[f'emb64_{i}']).max())
+        # random weights) are held to 1.5x that floor; the four north-star models to 1e-4
+        tol = max(TOL, 1.5 * helpers.rel_err(g[f'emb32_{i}'], g[f'emb64_{i}']).max())
         print(f'{arch} set{i}: rel err vs fp64 {e64:.2e}, vs reference fp32 {e32:.2e} (tol {tol:.1e})')
         assert e64 < tol and e32 < tol, (arch, i, e64, e32)
 
@@ -186,12 +186,20 @@ def test_variants_at_persistent_pw_sizes_vs_oracle(arch):
     with torch.no_grad():
         emb = m(x.cuda()).cpu().numpy()
     err = helpers.rel_err(emb, ref).max()
-    # as in the golden test: variants whose fp32 forward of these inputs is itself further than
-    # the bar from fp64 (huge 2.7e-4, w24s4ep4 6.7e-3) are held to twice that floor
-    floor = helpers.rel_err(models_ref.forward(arch, helpers.state_dict(arch), x).numpy(), ref).max()
-    tol = max(TOL, 2 * floor)
-    print(f'{arch} B={B} T={T}: rel err vs fp64 oracle {err:.2e} (fp32 floor {floor:.1e}, tol {tol:.1e})')
+    # variants whose fp32 forward of these inputs is itself further than the bar from fp64
+    # (huge 2.7e-4, w24s4ep4 6.7e-3) are held to 1.5x that floor against fp64.  Against the
+    # reference's own fp32 forward (oracle == reference to < 2e-6, test_oracle_models.py) the
+    # distance is bounded by both errors (triangle: up to 2.5x the floor); measured huge
+    # 3.83e-4 vs fp64, 4.34e-4 vs fp32 with a 2.7e-4 floor -- held to 2x the floor
+    ref32 = models_ref.forward(arch, helpers.state_dict(arch), x).numpy()
+    floor = helpers.rel_err(ref32, ref).max()
+    tol = max(TOL, 1.5 * floor)
+    tol32 = max(TOL, 2.0 * floor)
+    err32 = helpers.rel_err(emb, ref32).max()
+    print(f'{arch} B={B} T={T}: rel err vs fp64 {err:.2e}, vs reference fp32 {err32:.2e} '
+          f'(fp32 floor {floor:.1e}, tol {tol:.1e} / {tol32:.1e})')
     assert err < tol, (arch, err, tol)
+    assert err32 < tol32, (arch, err32, tol32)
 
 
 def test_plan_eviction_with_replays_on_two_streams():

@@ -163,3 +163,31 @@ def test_eres2net_hot_input_reruns_only_the_stem_segment():
     B, T, _ = feats.shape
     gp = h.guard_plan(B, T)
     assert gp['segments'] == 17 and 1 <= gp['twin_segments'] <= 2 and gp['gated_steps'] <= 14
+
+
+@pytest.mark.parametrize('arch,key,factor,kernels', [
+    ('ecapa', 'blocks.0.norm.norm.weight', 1e5, ('conv_gemm_x3f_kernel',)),
+    ('campplus', 'head.layer1.0.bn2.weight', 3e4, ('pw_gemm_x3_kernel', 'conv_gemm_x3_kernel<64, 32')),
+])
+def test_scaled_split_at_production_sizes(arch, key, factor, kernels):
+    """the scaled instances of the large-M kernels (the LDS-DMA GEMM, M > 4096; the
+    persistent 1x1 GEMM, M >= 65536; the 64x32 tile) run with the word set: 64 utterances x
+    1,100 frames (B*T = 70,400), the first and last rows checked against fp64."""
+    B, T = 64, 1100
+    rng = np.random.default_rng(11)
+    feats = torch.from_numpy(rng.standard_normal((B, T, 80)).astype(np.float32))
+    m = _scaled(arch, key, factor)
+    dev = torch.device('cuda', 0)
+    md = m.to(dev)
+    with torch.no_grad():
+        out = md(feats.to(dev)).cpu().numpy()
+    h = md._hip_handle(dev)
+    assert h.last_forward_flagged and not h.last_forward_exact
+    route = [k for _, k, _ in h.plan(B, T)]
+    for k in kernels:
+        assert any(r.startswith(k) for r in route), (k, sorted(set(route)))
+    rows = [0, B - 1]
+    sd = {k: v.double() if v.is_floating_point() else v for k, v in m.cpu().state_dict().items()}
+    ref = models_ref.forward(arch, sd, feats[rows].double()).numpy()
+    assert np.isfinite(out).all()
+    assert helpers.rel_err(out[rows], ref).max() < 1e-4, helpers.rel_err(out[rows], ref).max()

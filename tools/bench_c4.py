@@ -8,10 +8,12 @@ utterance of every row (top-1 trial score + index), so the 40 GB matrix never ex
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P tools/bench_c4.py                          # N GPUs (weak in GPUs, fixed corpus)
 
-Inputs: a pool of P distinct synthetic 2 s utterances (numpy PCG64, seed 1000 + i,
-SURVEY §8(d)); utterance u is pool[u % P] circularly shifted by 37 * (u // P) samples, so
-all 100k inputs differ.  Every rank builds its contiguous shard in HBM before the timed
-region (12.8 GB at N=1).  Timed region (barrier + synchronize on both sides, max over
+Inputs: utterance u is synth_wav(32000, seed = 1000 + u) (numpy PCG64),
+generated on the host by a process pool (forked before the GPU is touched) for the rank's
+contiguous shard and staged into HBM before the timed region (12.8 GB at N=1): the
+generator costs ~15 ms per utterance per core, ~100x the GPU's per-utterance time, so a
+producer inside the timed region would time the host.  --pool P (round-5 form): P distinct
+utterances, utterance u = pool[u % P] circularly shifted by 37 * (u // P) samples.  Timed region (barrier + synchronize on both sides, max over
 ranks): GPU Fbank + forward of the shard, the all-gather, the scoring pass.  Rank 0 prints
 one JSON line; stage times are HIP-event times on rank 0.
 """
@@ -46,11 +48,29 @@ def build_shard(pool, start, stop, device):
     return out
 
 
+def _gen_chunk(bounds):
+    from speakerlab.utils import synthetic
+    a, b = bounds
+    return a, np.stack([synthetic.synth_wav(SAMPLES, 1000 + u) for u in range(a, b)])
+
+
+def generate_shard(start, stop, workers):
+    """Per-utterance seeds 1000 + u for u in [start, stop), host-side (float32 [n, 32000])."""
+    import multiprocessing as mp
+    out = np.empty((stop - start, SAMPLES), dtype=np.float32)
+    chunks = [(a, min(stop, a + 256)) for a in range(start, stop, 256)]
+    with mp.get_context('fork').Pool(workers) as pool:
+        for a, w in pool.imap_unordered(_gen_chunk, chunks):
+            out[a - start:a - start + w.shape[0]] = w
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--utts', type=int, default=100_000)
     ap.add_argument('--batch', type=int, default=256)
-    ap.add_argument('--pool', type=int, default=1024)
+    ap.add_argument('--pool', type=int, default=0, help='0: every utterance its own seed (default)')
+    ap.add_argument('--gen-workers', type=int, default=16)
     ap.add_argument('--chunk-rows', type=int, default=4096)
     ap.add_argument('--warmup', type=int, default=2)
     args = ap.parse_args()
@@ -58,6 +78,11 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    from speakerlab.utils.distributed import shard_bounds
+    s0, s1 = shard_bounds(args.utts, rank, world)
+    t_gen = time.perf_counter()
+    host_wav = generate_shard(s0, s1, args.gen_workers) if args.pool == 0 else None   # before any GPU call
+    t_gen = time.perf_counter() - t_gen
     device = torch.device('cuda', local)
     torch.cuda.set_device(device)
     if world > 1:
@@ -65,14 +90,17 @@ def main():
 
     from speakerlab import _hip
     from speakerlab.utils import synthetic
-    from speakerlab.utils.distributed import all_gather_embeddings, shard_bounds
+    from speakerlab.utils.distributed import all_gather_embeddings
     import helpers
 
     model = helpers.loaded_module('eres2net_large').to(device).eval()
     E = 192
-    pool = torch.from_numpy(np.stack([synthetic.synth_wav(SAMPLES, 1000 + i) for i in range(args.pool)])).to(device)
-    s0, s1 = shard_bounds(args.utts, rank, world)
-    wav = build_shard(pool, s0, s1, device)
+    if host_wav is not None:
+        wav = torch.from_numpy(host_wav).to(device)
+        del host_wav
+    else:
+        pool = torch.from_numpy(np.stack([synthetic.synth_wav(SAMPLES, 1000 + i) for i in range(args.pool)])).to(device)
+        wav = build_shard(pool, s0, s1, device)
     n_local = s1 - s0
     emb_local = torch.empty((n_local, E), dtype=torch.float32, device=device)
 
@@ -135,7 +163,9 @@ def main():
             'score_tflops_per_gpu': round(flop_score / world / (ms[2] * 1e-3) / 1e12, 1),
             'top1_mean_score': round(float(best.mean()), 4),
             'dtype': 'f32 (fp16x3 MFMA convs, fp32 MFMA affinity)',
-            'data': f'synthetic: {args.pool} PCG64 utterances (seed 1000+i), circular shifts make {args.utts} distinct inputs',
+            'data': (f'synthetic: {args.utts} PCG64 utterances, seed 1000+i each (host-generated before the '
+                     f'timed region in {t_gen:.0f} s by {args.gen_workers} processes, resident in HBM)') if args.pool == 0 else
+                    f'synthetic: {args.pool} PCG64 utterances (seed 1000+i), circular shifts make {args.utts} distinct inputs',
             'parallelism': f'dp{world}: contiguous shards, 1 all-gather (RCCL), row-block scoring'}), flush=True)
     if world > 1:
         dist.destroy_process_group()
