@@ -108,11 +108,11 @@ struct ConvDesc {
 //    precision is that of the unscaled split.
 //    A loader that applies an affine pre-activation (CAM++ BN-ReLU, |relu(psc x + psh)| <=
 //    |psc| |x| + |psh|) breaks the 2x growth bound by up to P = max_c max(|psc|, |psh| / 2^14):
-//    with |x| < 2 max(word, 2^14) the operand is below 1.5 P 2^(e+2) (e: the word's exponent,
-//    13 when clear), so a further 2^-b with P <= 1.3 * 2^b keeps the scaled operand below
-//    2^15 again (host: pre_range_bits, ConvDesc::range_bits; applied in the twin plans too).  A block may read a larger word than another
-//    (producers of its own launch raising it meanwhile): each block undoes its own scale, so
-//    every output is consistent.
+//    with |x| < 2^(e+2) (e: the word's exponent, 13 when clear) the operand is below
+//    1.5 P 2^(e+2), so a further 2^-b with P <= 1.3 * 2^b keeps the scaled operand below
+//    1.95 * 2^15 < 65504 (host: pre_range_bits, ConvDesc::range_bits; applied in the twin
+//    plans too).  A block may read a larger word than another (producers of its own launch
+//    raising it meanwhile): each block undoes its own scale, so every output is consistent.
 constexpr float kRangeLimit = 16384.0f;
 // the tiled fp16x3 GEMM scales the weights' hi plane by 2^11 (conv_gemm.hip): 31.5 * 2^11 < 65504
 constexpr float kX3WeightLimit = 31.5f;

@@ -40,11 +40,15 @@
                         // on the 128 x 128 layers)
 #endif
 #ifndef SPK_F_M16
-#define SPK_F_M16 0   // 1: v_mfma_f32_16x16x32_f16 (fragments packed for it, epilogue_tiles L16 layout)
+#define SPK_F_M16 1   // 1: v_mfma_f32_16x16x32_f16 (round 6: 4-10 % faster per layer than 32x32x16, r06_ablation/m16_gemm.txt) (fragments packed for it, epilogue_tiles L16 layout)
+#endif
+#ifndef SPK_F_SKIP
+#define SPK_F_SKIP 1   // M16: skip the MFMAs of 16-column blocks past N
 #endif
 #ifndef SPK_FEXP
 #define SPK_FEXP 0   // ablation builds only (tools/fexp.sh), bit mask: 1 no MFMA, 2 no in-loop A loads,
-                     // 4 no in-loop A split / stores, 8 no in-loop B DMA, 16 no epilogue stores
+                     // 4 no in-loop A split / stores, 8 no in-loop B DMA, 16 no epilogue (accumulators
+                     // summed), 32 epilogue without its residual loads
 #endif
 
 namespace spk {
@@ -278,6 +282,9 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
 #pragma unroll
     for (int j = 0; j < 2 * TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   f16x8 bh[2 * TN], bl[2 * TN], bh2[2 * TN];
+  // columns of the packed N (padded to 256) this wave's tile actually holds: the MFMAs of
+  // 16-column blocks past N are skipped (N = 104 / 208 / 416 fill 81 % of their 128 / 256 tiles)
+  const int ncols = __builtin_amdgcn_readfirstlane(d.N - (n0 + wn * TN * 32));
   auto compute_s = [&](int buf, int s) {
     const _Float16* ahi = reinterpret_cast<const _Float16*>(lb + buf * C::STAGE);
     if (s == 0) {
@@ -297,6 +304,9 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
       const f16x8 al = *reinterpret_cast<const f16x8*>(p + C::PA);
 #pragma unroll
       for (int j = 0; j < 2 * TN; ++j) {
+#if SPK_F_SKIP
+        if (j * 16 >= ncols) continue;                   // a 16-column block wholly past N (wave-uniform)
+#endif
         if (SPK_FEXP & 1) {
           acc[i][j][0] += (float)ah[0] + (float)bh2[j][1] + (float)bl[j][2] + (float)al[3] + (float)bh[j][4];
           continue;
@@ -457,12 +467,16 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
   const float back = pow2_div(sc, -11);               // 2^(-11) / sc, exact
 #if SPK_F_M16
   // the four 16x16 accumulators of 32x32 tile (i, j) as one f32x16 (epilogue_tiles L16)
+#pragma unroll
+  for (int i = 0; i < 2 * TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2 * TN; ++j) acc[i][j] *= back;
   auto tile = [&](int i, int j) {
     f32x16 t;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) t[4 * q + e] = acc[2 * i + (q >> 1)][2 * j + (q & 1)][e] * back;
+      for (int e = 0; e < 4; ++e) t[4 * q + e] = acc[2 * i + (q >> 1)][2 * j + (q & 1)][e];
     return t;
   };
   constexpr bool L16 = true;
@@ -476,10 +490,25 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
 #endif
 #if SPK_FEXP & 16
   {
-    const f32x16 t0 = tile(0, 0), t1 = tile(TM - 1, TN - 1);
-    if (t0[0] == 1234.5f && t1[3] == 77.f) d.out[tid] = t0[1];
+    // every accumulator stays live (a test of two elements let the compiler drop the MFMAs of
+    // all other tiles: the round-5 form of this ablation measured that, not the epilogue)
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const f32x16 t = tile(i, j);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sum += t[r];
+      }
+    if (sum == 1234.5f) d.out[tid] = sum;
   }
 #else
+#if SPK_FEXP & 32
+  ConvDesc dnores = d;                                   // ablation: epilogue without its residual loads
+  dnores.res = nullptr;
+#define d dnores
+#endif
   // one row of accumulator tiles at a time through the wave's slab (TN x 4 KB): the whole
   // wave tile of a 256-wide block would not fit in LDS
   if constexpr (C::EPI_ONE) {
@@ -504,6 +533,9 @@ conv_gemm_x3f_kernel(const ConvDesc d) {
                                                     [&](int r) { return rb + r; });
   };
   StaticFor<0, TM>::run(epi_row);
+#if SPK_FEXP & 32
+#undef d
+#endif
 #endif
 }
 

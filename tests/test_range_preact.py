@@ -75,7 +75,7 @@ def test_construction_overflows_the_word_only_scale(factor):
     assert amax * 2.0 ** -s > 65504            # the round-5 scale saturates this operand
     b = _pre_range_bits(P)
     assert b >= 3
-    assert amax * 2.0 ** -(s + b) < 2.0 ** 15   # the pre-activation bits bring it back in range
+    assert amax * 2.0 ** -(s + b) < 1.95 * 2.0 ** 15   # the pre-activation bits bring it back in range (common.h)
     if factor == 3e3:
         assert word < RANGE_LIMIT               # ... even with the word clear (sc = 1 before)
 

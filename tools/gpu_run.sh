@@ -34,6 +34,7 @@ if phase tests || phase core; then
   if fatal $rc; then exit $rc; fi
 fi
 if phase gemm; then
+  [ tools/gemm_bench -nt 3d-speaker_amd/csrc/common.h ] || { echo "gemm_bench older than common.h: rebuild it"; exit 2; }
   echo "== gemm_bench $(date +%T)"
   timeout -k 10 600 tools/gemm_bench --reps ${REPS:-20} ${SHAPES:+--shapes $SHAPES} ${LIBS} > gpurun_out/${TAG}_gemm.txt 2>&1
   rc=$?; echo "gemm rc=$rc"; cat gpurun_out/${TAG}_gemm.txt | tail -${NTAIL:-60}
