@@ -26,6 +26,6 @@ struct AffDesc {
 // true when launch_aff_x3 serves this geometry (fp16x3 path on, nmid 32 / 64, cp % 8 == 0)
 bool aff_x3_supported(int cp, int nmid);
 hipError_t launch_aff_x3(const AffDesc& a, hipStream_t s);
-std::string aff_x3_kernel_name(int nmid);
+std::string aff_x3_kernel_name(int cp, int nmid);
 
 }  // namespace spk

@@ -24,6 +24,7 @@
 
 #include "aff.h"
 #include "conv_epilogue.h"
+#include "conv_loader.h"
 
 namespace spk {
 
@@ -31,6 +32,7 @@ namespace {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void split8(const f32x4 a, const f32x4 b, f16x8& hi, f16x8& lo) {
   h16x4 ha, la, hb, lb;
@@ -217,6 +219,209 @@ __global__ void __launch_bounds__(256) aff_x3_kernel(const AffDesc a) {
   range_note(a.range_flag, amax);
 }
 
+// ---------------------------------------------------------------------------------------
+// Persistent form for a 32-channel bottleneck and cp <= 128 (ERes2NetV2 / ERes2Net layer-3
+// fusions), round 6.  The kernel above is latency-bound (2.2 TB/s, MFMA busy 0.05): each of
+// its stage-1 k-steps waits for that step's [x | y] loads (one step ahead) and W1 fragment
+// loads, and the combine re-reads x / y from L2.  Here
+//   * W1 and W2 live in LDS (loaded once per block, fp16 hi / lo planes, rows padded to 40
+//     halves: conflict-free ds_read_b128), so no global load sits inside the MFMA chains;
+//   * a wave owns 16 pixels at a time on v_mfma_f32_16x16x32_f16 (transposed GEMMs, pixels
+//     along the MFMA columns) and walks tiles with a stride of the grid; 16 waves per CU
+//     (two 8-wave blocks) keep 16 tiles' x / y in flight;
+//   * the K order of stage 1 is permuted so that lane (pixel l & 15, group g = l >> 4) loads,
+//     for each 32-channel group c of x and of y, channels 32c + 4g .. +3 and 32c + 16 + 4g .. +3
+//     -- exactly the channels stage 2's accumulators give that lane (n = 16 nb + 4g + e), so the
+//     combine takes x and y from the same registers: HBM traffic is x, y and out once each;
+//   * stage 1's accumulators (lane: pixel, j = 16 jb + 4g + e) are stage 2's B operand under
+//     the matching permutation of W2's columns (k slot 8g + e <-> j = 4g + e, 16 + 4g + e - 4).
+// fp16x3 products and the two-accumulator order as aff_x3_kernel.
+constexpr int AP_ROW = 40;   // halves per LDS weight row (32 + 8: conflict-free b128 reads)
+
+// CX 32-channel groups of x (and of y), the last one with LH valid 16-channel halves:
+// cp <= 32 (CX - 1) + 16 LH (ERes2NetV2 layer 3: cp = 104, CX = 4, LH = 1)
+template <int CX, int LH>
+__global__ void __launch_bounds__(512, 4) aff_x3p_kernel(const AffDesc a) {   // 4 waves per SIMD
+  constexpr int KS1 = 2 * CX;                       // stage-1 k-steps (x groups, then y groups)
+  constexpr int NB = 2 * (CX - 1) + LH;             // stage-2 16-channel output blocks
+  extern __shared__ float aff_lds[];
+  _Float16* const w1h = reinterpret_cast<_Float16*>(aff_lds);          // [KS1][32][AP_ROW]
+  _Float16* const w1l = w1h + KS1 * 32 * AP_ROW;
+  _Float16* const w2h = w1l + KS1 * 32 * AP_ROW;                      // [16 NB][AP_ROW]
+  _Float16* const w2l = w2h + NB * 16 * AP_ROW;
+  float* const b2s = reinterpret_cast<float*>(w2l + NB * 16 * AP_ROW);        // [16 NB]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int cp = a.cp;
+
+  // ---- weights -> LDS in the permuted K orders (zeros past cp / nmid).  Slot kk = 8 gg + e of
+  // a 32-deep step holds channel 4 gg + e (e < 4) or 16 + 4 gg + e - 4: two 4-half runs, each
+  // one 8-byte load; every load of the staging is issued before the first LDS store (a
+  // load-store loop paid one L2 round trip per element at kernel start: ~30 us per launch)
+  typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+  {
+    constexpr int N1 = KS1 * 32 * 8;                // W1 runs: (step c, row j, run r = 2 gg + half)
+    constexpr int N2 = NB * 16 * 8;                 // W2 runs: (row n, run)
+    constexpr int R1 = (N1 + 511) / 512, R2 = (N2 + 511) / 512;
+    u16x4 h1[R1], l1[R1], h2[R2], l2[R2];
+#pragma unroll
+    for (int r = 0; r < R1; ++r) {
+      const int i = tid + 512 * r;
+      const int run = i & 7, j = (i >> 3) & 31, c = min(i >> 8, KS1 - 1);
+      const int ch = 32 * (c % CX) + (run & 1) * 16 + 4 * (run >> 1);
+      const bool ok = i < N1 && ch < cp;
+      const size_t o = (size_t)j * a.kp1 + (c < CX ? 0 : cp) + (ok ? ch : 0);
+      h1[r] = *reinterpret_cast<const u16x4*>(a.w1h + o);
+      l1[r] = *reinterpret_cast<const u16x4*>(a.w1l + o);
+      if (!ok) h1[r] = l1[r] = u16x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int r = 0; r < R2; ++r) {
+      const int i = tid + 512 * r;
+      const int run = i & 7, n = min(i >> 3, NB * 16 - 1);
+      const int jj = (run & 1) * 16 + 4 * (run >> 1);
+      const bool ok = i < N2 && n < cp;
+      const size_t o = (size_t)(ok ? n : 0) * a.kp2 + jj;
+      h2[r] = *reinterpret_cast<const u16x4*>(a.w2h + o);
+      l2[r] = *reinterpret_cast<const u16x4*>(a.w2l + o);
+      if (!ok) h2[r] = l2[r] = u16x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int r = 0; r < R1; ++r) {
+      const int i = tid + 512 * r;
+      if (i >= N1) continue;
+      const int run = i & 7, j = (i >> 3) & 31, c = i >> 8;
+      const int kk = 8 * (run >> 1) + 4 * (run & 1);
+      *reinterpret_cast<u16x4*>(w1h + (c * 32 + j) * AP_ROW + kk) = h1[r];
+      *reinterpret_cast<u16x4*>(w1l + (c * 32 + j) * AP_ROW + kk) = l1[r];
+    }
+#pragma unroll
+    for (int r = 0; r < R2; ++r) {
+      const int i = tid + 512 * r;
+      if (i >= N2) continue;
+      const int run = i & 7, n = i >> 3;
+      const int kk = 8 * (run >> 1) + 4 * (run & 1);
+      *reinterpret_cast<u16x4*>(w2h + n * AP_ROW + kk) = h2[r];
+      *reinterpret_cast<u16x4*>(w2l + n * AP_ROW + kk) = l2[r];
+    }
+  }
+  for (int i = tid; i < NB * 16; i += 512) b2s[i] = i < cp ? a.b2[i] : 0.f;
+  // stage-1 bias of this lane's bottleneck channels j = 4g + e and 16 + 4g + e
+  const f32x4 b1a = *reinterpret_cast<const f32x4*>(a.b1 + 4 * g);
+  const f32x4 b1b = *reinterpret_cast<const f32x4*>(a.b1 + 16 + 4 * g);
+  __syncthreads();
+
+  const int ntiles = (a.M + 15) / 16;
+  const int wstride = gridDim.x * 8;
+  const int t0 = blockIdx.x * 8 + wave;
+  // x / y quads of a tile: [c][h] = channels 32c + 16h + 4g .. +3 of pixel 16 t + l16 (clamped
+  // row, clamped in-row column: every load unconditional; channels past cp meet zero weights
+  // and are never stored)
+  struct XY {
+    f32x4 x[CX][2], y[CX][2];
+  };
+  auto load = [&](int t, XY& v) {
+    const int m = min(16 * t + l16, a.M - 1);
+    const float* xr = a.x + (size_t)m * a.ldx;
+    const float* yr = a.y + (size_t)m * a.ldy;
+#pragma unroll
+    for (int c = 0; c < CX; ++c)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (c == CX - 1 && h >= LH) {               // past cp for every lane: not loaded
+          v.x[c][h] = v.y[c][h] = f32x4{0.f, 0.f, 0.f, 0.f};
+          continue;
+        }
+        const int ch = min(32 * c + 16 * h + 4 * g, cp - 4);
+        v.x[c][h] = *reinterpret_cast<const f32x4*>(xr + ch);
+        v.y[c][h] = *reinterpret_cast<const f32x4*>(yr + ch);
+      }
+  };
+  float amax = 0.f;
+  auto tile = [&](int t, const XY& v) {
+    // stage 1: hT[j][m] over K = [x | y] (permuted), two 16-row j blocks
+    f32x4 h[2], hx[2];
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) { h[jb] = f32x4{0.f, 0.f, 0.f, 0.f}; hx[jb] = h[jb]; }
+#pragma unroll
+    for (int c = 0; c < KS1; ++c) {
+      const int cc = c % CX;
+      const bool isx = c < CX;
+      f32x4 q0 = isx ? v.x[cc][0] : v.y[cc][0], q1 = isx ? v.x[cc][1] : v.y[cc][1];
+      // channels past cp: zero (their W1 columns are zero too, but the clamped load may hold
+      // finite garbage from the row's tail -- keep the products exactly zero)
+      if (32 * cc + 4 * g >= cp) q0 = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (32 * cc + 16 + 4 * g >= cp) q1 = f32x4{0.f, 0.f, 0.f, 0.f};
+      h16x4 h0, l0, h1, l1;
+      split_x3(q0, h0, l0);
+      split_x3(q1, h1, l1);
+      const f16x8 bh = f16x8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+      const f16x8 bl = f16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        const int o = (c * 32 + 16 * jb + l16) * AP_ROW + 8 * g;
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(w1h + o);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(w1l + o);
+        h[jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, h[jb], 0, 0, 0);
+        hx[jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, hx[jb], 0, 0, 0);
+        hx[jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, hx[jb], 0, 0, 0);
+      }
+    }
+    // bias + SiLU, split: stage 2's B operand (k slot 8g + e: j = 4g + e, then 16 + 4g + e)
+    f16x8 gh, gl;
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float z = h[jb][e] + hx[jb][e] * (1.0f / 2048.0f) + (jb ? b1b[e] : b1a[e]);
+        z = z * __builtin_amdgcn_rcpf(1.0f + __expf(-z));   // SiLU (hardware reciprocal)
+        const _Float16 zh = (_Float16)z;
+        gh[4 * jb + e] = zh;
+        gl[4 * jb + e] = (_Float16)((z - (float)zh) * 2048.0f);
+      }
+    // stage 2 + combine, one 16-channel output block at a time
+    const int m = 16 * t + l16;
+    // stores through a resource based at the tile's first row: a lane past M or cp gets an
+    // offset the buffer unit drops, so no store (and no load) sits behind a branch
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + (size_t)16 * t * a.ldo);
+    const uint32_t orow = m < a.M ? (uint32_t)l16 * (uint32_t)a.ldo * 4u : BUF_OOB;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int o = (nb * 16 + l16) * AP_ROW + 8 * g;
+      const f16x8 ah = *reinterpret_cast<const f16x8*>(w2h + o);
+      const f16x8 al = *reinterpret_cast<const f16x8*>(w2l + o);
+      f32x4 z = {0.f, 0.f, 0.f, 0.f}, zx = z;
+      z = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, gh, z, 0, 0, 0);
+      zx = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, gl, zx, 0, 0, 0);
+      zx = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, gh, zx, 0, 0, 0);
+      const int n = 16 * nb + 4 * g;                  // this lane's four output channels
+      const f32x4 xv = v.x[nb >> 1][nb & 1], yv = v.y[nb >> 1][nb & 1];
+      const f32x4 b2 = *reinterpret_cast<const f32x4*>(b2s + n);
+      f32x4 out;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        // x(1 + tanh z) + y(1 - tanh z) = 2(y + s(x - y)), s = sigmoid(2z): one exp + rcp
+        const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * (z[e] + zx[e] * (1.0f / 2048.0f) + b2[e])));
+        out[e] = 2.0f * fmaf(sg, xv[e] - yv[e], yv[e]);
+      }
+      const bool ok = n < cp && orow != BUF_OOB;
+      if (ok) amax = fmaxf(amax, fmaxf(fmaxf(fabsf(out[0]), fabsf(out[1])), fmaxf(fabsf(out[2]), fabsf(out[3]))));
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, out), ro, ok ? (int)(orow + 4u * n) : (int)BUF_OOB, 0, 0);
+    }
+  };
+  // persistent walk; one register set per wave (a second one, for a prefetch of the next
+  // tile, spills at CX = 4): the memory parallelism comes from 16 waves per CU instead
+  for (int t = t0; t < ntiles; t += wstride) {
+    XY v;
+    load(t, v);
+    // all of the tile's loads issued before any use (left to itself the scheduler sank them
+    // next to their uses, one vmcnt(0) round trip per load)
+    __builtin_amdgcn_sched_barrier(0);
+    tile(t, v);
+  }
+  range_note(a.range_flag, amax);
+}
+
 }  // namespace
 
 bool aff_x3_supported(int cp, int nmid) {
@@ -229,7 +434,23 @@ bool aff_x3_supported(int cp, int nmid) {
   return !off && conv_use_x3() && (nmid == 32 || nmid == 64) && cp % 8 == 0 && cp >= 8 && cp <= 208;
 }
 
-std::string aff_x3_kernel_name(int nmid) { return "aff_x3_kernel<" + std::to_string(nmid / 32) + ">"; }
+// the persistent form (aff_x3p_kernel): a 32-channel bottleneck, cp <= 128;
+// SPK_AFF_P=0 keeps aff_x3_kernel (A/B runs)
+bool aff_p_ok(int cp, int nmid) {
+  static const bool off = [] {
+    const char* e = std::getenv("SPK_AFF_P");
+    return e && std::atoi(e) == 0;
+  }();
+  return !off && nmid == 32 && cp <= 128 && cp % 8 == 0;
+}
+
+std::string aff_x3_kernel_name(int cp, int nmid) {
+  if (aff_p_ok(cp, nmid)) {
+    const int cx = (cp + 31) / 32;
+    return "aff_x3p_kernel<" + std::to_string(cx) + ", " + (cp - 32 * (cx - 1) <= 16 ? "1" : "2") + ">";
+  }
+  return "aff_x3_kernel<" + std::to_string(nmid / 32) + ">";
+}
 
 hipError_t launch_aff_x3(const AffDesc& a, hipStream_t s) {
   // host-side shape checks: every vector access stays aligned and inside its row
@@ -250,6 +471,19 @@ hipError_t launch_aff_x3(const AffDesc& a, hipStream_t s) {
     const char* e = std::getenv("SPK_AFF_LDS_KB");
     return std::max((size_t)(e ? std::atoi(e) : 60) * 1024, (size_t)4 * 32 * SLAB_LD * sizeof(float));
   }();
+  if (aff_p_ok(a.cp, a.nmid)) {
+    const int cx = (a.cp + 31) / 32;
+    const size_t lds = ((size_t)2 * cx * 32 * AP_ROW * 2 + (size_t)2 * cx * 16 * AP_ROW * 2) * sizeof(_Float16) +
+                       (size_t)2 * cx * 16 * sizeof(float);
+    const int ntiles = (a.M + 15) / 16;
+    const int blocks = std::max(1, std::min((ntiles + 7) / 8, 2 * device_cus()));
+    const int lh = a.cp - 32 * (cx - 1) <= 16 ? 1 : 2;
+#define SPK_AFFP(CX, LH) if (cx == CX && lh == LH) hipLaunchKernelGGL((aff_x3p_kernel<CX, LH>), dim3(blocks), dim3(512), lds, s, a)
+    SPK_AFFP(1, 1); SPK_AFFP(1, 2); SPK_AFFP(2, 1); SPK_AFFP(2, 2);
+    SPK_AFFP(3, 1); SPK_AFFP(3, 2); SPK_AFFP(4, 1); SPK_AFFP(4, 2);
+#undef SPK_AFFP
+    return hipGetLastError();
+  }
   if (a.nmid == 32) hipLaunchKernelGGL(aff_x3_kernel<1>, grid, block, lds_pad, s, a);
   else hipLaunchKernelGGL(aff_x3_kernel<2>, grid, block, lds_pad, s, a);
   return hipGetLastError();

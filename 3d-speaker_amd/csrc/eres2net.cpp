@@ -177,7 +177,7 @@ struct ERes2Builder {
         ad.out = c.resolve(ob);
         ad.range_flag = c.flag;
         return launch_aff_x3(ad, c.stream);
-      }, aff_x3_kernel_name(mid.n_phys), bytes);
+      }, aff_x3_kernel_name(cp, mid.n_phys), bytes);
       return bout;
     }
     b.macs_per_utt += m0;

@@ -119,7 +119,7 @@ std::string conv_kernel_name(const ConvDesc&) { return "emu_conv"; }
 // fused AFF (aff.hip contract): h = SiLU(W1 [x|y] + b1), z = W2 h + b2,
 // out = x (1 + tanh z) + y (1 - tanh z); fp32 weights, double accumulation
 bool aff_x3_supported(int cp, int nmid) { return (nmid == 32 || nmid == 64) && cp % 8 == 0 && cp >= 8 && cp <= 208; }
-std::string aff_x3_kernel_name(int nmid) { return "emu_aff<" + std::to_string(nmid / 32) + ">"; }
+std::string aff_x3_kernel_name(int, int nmid) { return "emu_aff<" + std::to_string(nmid / 32) + ">"; }
 hipError_t launch_aff_x3(const AffDesc& a, hipStream_t) {
   EMU_GATE();
   if (!aff_x3_supported(a.cp, a.nmid) || a.kp1 < 2 * a.cp || a.kp2 < a.nmid) return hipErrorInvalidValue;
