@@ -64,7 +64,7 @@ void build_campplus(Builder& b, int T) {
     const Buf xo = x.buf;
     const bool rg = b.ragged;
     const bool flag = !b.exact;
-    b.step("head.stem", [=](const Ctx& c) {
+    b.writes({{xo, Builder::NOTED}}).step("head.stem", [=](const Ctx& c) {
       return launch_stem_conv3x3(c.in, B, T, F, w, bias, mc, ACT_RELU, kp, c.resolve(xo), mc, c.stream,
                                  rg ? c.lens : nullptr, flag ? c.flag : nullptr);
     });
@@ -169,7 +169,7 @@ void build_campplus(Builder& b, int T) {
     LEN2 = b.alloc((size_t)B);
     if (b.plan) {
       const int pad = K5 / 2, k5 = K5;
-      b.step("xvector.tdnn.lengths", [=](const Ctx& c) {
+      b.writes({{LEN2, Builder::AUX}}).step("xvector.tdnn.lengths", [=](const Ctx& c) {
         return launch_derive_len(c.lens, c.resolve_i(LEN2), B, pad, k5, 2, c.stream);
       });
     }
@@ -263,7 +263,7 @@ void build_campplus(Builder& b, int T) {
         const float* b2 = cl2.has_bias ? m.dptr(cl2.b_off) : nullptr;
         const int k1p = cl1.Kp, k2p = cl2.Kp;
         b.macs_per_utt += m_c1 + m_c2;
-        b.step(c + ".gate", [=](const Ctx& cx) {
+        b.writes({{GATE, Builder::AUX}, {SEGSUM, Builder::AUX}}).step(c + ".gate", [=](const Ctx& cx) {
           return launch_cam_gate(cx.resolve(Hh), B, T2, bnc, bnc, 100, nseg, w1, k1p, b1, red, w2, k2p, b2, growth,
                                  cx.resolve(GATE), growth, cx.resolve(SEGSUM), cx.stream, cx.resolve_i(LEN2));
         }, "cam_gate_kernel", 4.0 * B * T2 * bnc);
@@ -324,7 +324,7 @@ void build_campplus(Builder& b, int T) {
                             2 * c_final);
   b.macs_per_utt += (double)E * 2 * c_final;
   if (!b.plan) return;
-  b.step("xvector.stats", [=](const Ctx& c) {
+  b.writes({{ST, Builder::BOUNDED}}).step("xvector.stats", [=](const Ctx& c) {
     return launch_stats_pool(c.resolve(xo_final), B, T2, c_final, c_final, c.resolve(ST), c.stream,
                              c.resolve_i(LEN2));
   });

@@ -195,7 +195,7 @@ void build_ecapa(Builder& b, int T) {
                                 {Part{q + ".conv2.conv.weight", q + ".conv2.conv.bias", "", ChanMap::dense(se), 0, 0}}, se);
       b.macs_per_utt += 2.0 * Ci * se;
       if (b.plan) {
-        b.step(q + ".mean", [=](const Ctx& c) { return launch_time_mean(c.resolve(H2), B, T, Ci, Ci, c.resolve(S), Ci, c.stream, c.resolve_i(LENS)); });
+        b.writes({{S, Builder::BOUNDED}}).step(q + ".mean", [=](const Ctx& c) { return launch_time_mean(c.resolve(H2), B, T, Ci, Ci, c.resolve(S), Ci, c.stream, c.resolve_i(LENS)); });
         ConvDesc d1;
         d1.nimg = B; d1.Ho = 1; d1.Wo = 1;
         d1.s0 = src_vec(Ci);
@@ -209,7 +209,7 @@ void build_ecapa(Builder& b, int T) {
         Builder::ConvIO io2; io2.s0 = S1; io2.out = G;
         b.conv(q + ".conv2", d2, p2, io2);
         const Buf out = CATB.at((size_t)cat_off);
-        b.step(p + ".se_apply", [=](const Ctx& c) {
+        b.writes({{out, Builder::NOTED}}).step(p + ".se_apply", [=](const Ctx& c) {
           return launch_se_apply(c.resolve(H2), Ci, c.resolve(G), Ci, c.resolve(res), res_ld, c.resolve(out), catC, B, T,
                                  Ci, c.stream, c.flag);
         });
@@ -264,7 +264,7 @@ void build_ecapa(Builder& b, int T) {
     b.macs_per_utt += macs_ctx + macs_att + macs_conv + macs_fc;
     return;
   }
-  b.step("asp.stats", [=](const Ctx& c) { return launch_asp_stats(c.resolve(A), B, T, Cm, Cm, 1e-12f, c.resolve(MS), c.stream, c.resolve_i(LENS)); });
+  b.writes({{MS, Builder::BOUNDED}}).step("asp.stats", [=](const Ctx& c) { return launch_asp_stats(c.resolve(A), B, T, Cm, Cm, 1e-12f, c.resolve(MS), c.stream, c.resolve_i(LENS)); });
   {
     ConvDesc d;
     d.nimg = B; d.Ho = 1; d.Wo = 1;
@@ -294,7 +294,7 @@ void build_ecapa(Builder& b, int T) {
     b.macs_per_utt += macs_conv;
     b.conv("asp.conv", d, patt2, io);
   }
-  b.step("asp.pool", [=](const Ctx& c) {
+  b.writes({{P, Builder::BOUNDED}}).step("asp.pool", [=](const Ctx& c) {
     return launch_attn_pool(c.resolve(L), Cm, c.resolve(A), Cm, B, T, Cm, 1e-12f, c.resolve(P), c.stream,
                             c.resolve_i(LENS));
   });

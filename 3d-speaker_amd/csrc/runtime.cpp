@@ -196,8 +196,42 @@ void Builder::segment(bool twin) {
   plan->seg_twin.push_back(twin ? 1 : 0);
 }
 
+namespace {
+// the allocation (Plan::allocs entry) holding workspace byte offset `off`, or SIZE_MAX
+size_t alloc_of(const Plan& p, size_t off) {
+  size_t best = SIZE_MAX;
+  for (const auto& a : p.allocs)
+    if (a.first <= off && off < a.first + std::max<size_t>(a.second, 1) * sizeof(float)) best = a.first;
+  return best;
+}
+}  // namespace
+
+void Builder::record_write(const Buf& b, Grow g) {
+  if (!plan || b.kind != Buf::WS) return;
+  const size_t a = alloc_of(*plan, b.off);
+  if (a == SIZE_MAX) throw SpkError(SPK_E_INVALID, "internal: write outside every workspace allocation");
+  alloc_writers[a] |= 1 << g;
+}
+
+void Builder::check_operand(const std::string& name, const Buf& b) const {
+  if (!plan || !scaled || b.kind != Buf::WS) return;   // model input: the range_in step notes it
+  const size_t a = alloc_of(*plan, b.off);
+  const auto it = alloc_writers.find(a);
+  const int w = a == SIZE_MAX || it == alloc_writers.end() ? 0 : it->second;
+  if (!w || (w & (1 << AUX)))
+    throw SpkError(SPK_E_INVALID, "internal: scaled-split operand of " + name +
+                                      " has no declared NOTED / BOUNDED producer (runtime.h Builder::writes)");
+}
+
 void Builder::step(const std::string& name, Step s, const std::string& kernel, double bytes) {
+  const bool declared = writes_declared;
+  const std::vector<Write> w = std::move(pending_writes);
+  pending_writes.clear();
+  writes_declared = false;
   if (!plan) return;
+  if (scaled && !declared)
+    throw SpkError(SPK_E_INVALID, "internal: step " + name + " of a scaled plan without declared writes");
+  for (const Write& x : w) record_write(x.buf, x.grow);
   plan->steps.push_back(std::move(s));
   plan->names.push_back(name);
   plan->kernels.push_back(kernel.empty() ? name : kernel);
@@ -263,6 +297,11 @@ void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const C
   if (io.s1) bytes += 4.0 * px_out * d.s1.cin;
   if (io.res) bytes += 4.0 * px_out * d.N;
   if (io.affx) bytes += 8.0 * px_out * d.N;
+  check_operand(name, io.s0);
+  check_operand(name, io.s0b);
+  check_operand(name, io.s1);
+  // the epilogue notes the output in the range word whenever the plan is not exact
+  writes({Write{io.out, guard ? NOTED : AUX}});
   step(name, [d, cio, guard, scale_in](const Ctx& c) mutable {
     d.range_flag = guard ? c.flag : nullptr;
     d.range_in = scale_in ? c.flag : nullptr;
@@ -376,7 +415,7 @@ std::unique_ptr<Plan> build_plan(spk_model_t* h, int B, int T, bool ragged, bool
   if (!exact) {
     // fp16x3 range guard on the model input (common.h)
     const size_t n = (size_t)B * T * h->m.cfg.feat_dim;
-    b.step("range_in", [n](const Ctx& c) { return launch_range_check(c.in, n, c.flag, c.stream); });
+    b.writes({}).step("range_in", [n](const Ctx& c) { return launch_range_check(c.in, n, c.flag, c.stream); });
   }
   switch (h->m.cfg.arch) {
     case SPK_ARCH_ERES2NETV2: build_eres2net(b, T, true); break;

@@ -186,6 +186,29 @@ struct Builder {
   bool x3() const { return !exact && conv_use_x3(); }
   Buf alloc(size_t floats);
   void step(const std::string& name, Step s, const std::string& kernel = "", double bytes = 0.0);
+  // Scaled-split invariant (common.h): every split-GEMM operand is at most 2x the largest value
+  // an earlier producer noted in the range word.  In a scaled plan every non-conv step declares
+  // the workspace buffers it writes before it is emitted (`writes(...).step(...)`): NOTED (its
+  // kernel raises the word, like every conv epilogue), BOUNDED (its outputs stay within 2x of
+  // its inputs' largest value: means, standard deviations, gates) or AUX (lengths, gates and
+  // partial sums that no GEMM reads as an operand).  Builder::conv then refuses an operand
+  // whose allocation has an AUX writer or no declared writer at all (SpkError at plan build),
+  // so a future amplifying step cannot feed a split GEMM unnoticed.
+  enum Grow { NOTED = 0, BOUNDED = 1, AUX = 2 };
+  struct Write {
+    Buf buf;
+    Grow grow;
+  };
+  Builder& writes(std::vector<Write> w) {
+    pending_writes = std::move(w);
+    writes_declared = true;
+    return *this;
+  }
+  std::vector<Write> pending_writes;
+  bool writes_declared = false;
+  std::map<size_t, int> alloc_writers;   // allocation offset -> OR of (1 << Grow) of its writers
+  void record_write(const Buf& b, Grow g);
+  void check_operand(const std::string& name, const Buf& b) const;
   // close a range-guard segment at the current step (Plan::seg_end); `twin`: the gated
   // exact twin of the segment must run behind it (models without segments: one segment, twin)
   void segment(bool twin);
