@@ -236,7 +236,8 @@ __global__ void __launch_bounds__(256) aff_x3_kernel(const AffDesc a) {
 //   * stage 1's accumulators (lane: pixel, j = 16 jb + 4g + e) are stage 2's B operand under
 //     the matching permutation of W2's columns (k slot 8g + e <-> j = 4g + e, 16 + 4g + e - 4).
 // fp16x3 products and the two-accumulator order as aff_x3_kernel.
-constexpr int AP_ROW = 40;   // halves per LDS weight row (32 + 8: conflict-free b128 reads)
+constexpr int AP_ROW = 48;   // halves per LDS weight row (96 B: the 16x16x32 fragment reads of one ds_read_b128
+                             // lane group land on distinct banks, conv_gemm_f.hip FCfg::LROW)
 
 // CX 32-channel groups of x (and of y), the last one with LH valid 16-channel halves:
 // cp <= 32 (CX - 1) + 16 LH (ERes2NetV2 layer 3: cp = 104, CX = 4, LH = 1)

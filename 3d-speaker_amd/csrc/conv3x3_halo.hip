@@ -26,6 +26,9 @@
 #ifndef SPK_EXP
 #define SPK_EXP 0
 #endif
+#ifndef SPK_HALO_M16
+#define SPK_HALO_M16 1   // x3 kernel on v_mfma_f32_16x16x32_f16 (round 6; 0: 32x32x16)
+#endif
 #ifndef SPK_HALO_PF2
 #define SPK_HALO_PF2 0   // two halos in flight: measured neutral on ERes2NetV2, slower on ERes2Net-large / CAM++
 #endif
@@ -319,14 +322,24 @@ conv3x3_halo_persistent_kernel(const ConvDesc d) {
 template <int CIN, int PIX, int KS, int SH = 1>
 struct HaloX3Cfg {
   static constexpr int NP = 32, NW = PIX / 32, NT = 64 * NW * KS;
-  static constexpr int CINP = (CIN + 15) / 16 * 16, ROW = CINP + 8, QP = CINP / 4, Q = CIN / 4;
+  static constexpr int CINP = (CIN + 15) / 16 * 16, QP = CINP / 4, Q = CIN / 4;
   static constexpr int KSTEPS = CINP / 16, KSG = KSTEPS / KS;       // k-steps per tap / per group
+  // 16x16x32 form where a group's tap is whole 32-deep steps (not the SH = 2 form, KSG = 1)
+  // and two k-groups (52 / 64 channels): the one-group forms (28 / 32 channels) would need 92
+  // instead of 76 KB of LDS for the wider rows, one block per CU instead of two (CAM++ FCM halo
+  // launches 1.29 -> 1.76 ms, r06_ablation/halo_m16_ab.txt)
+  static constexpr bool M16 = SPK_HALO_M16 != 0 && KSG % 2 == 0 && KS == 2;
+  // pixel / weight rows: CINP + 8 halves (conflict-free for the 32x32x16 reads); the 16x16x32
+  // reads (lane: row l & 15, 16-B block l >> 4; ds_read_b128 lane groups {0-3, 12-15, 20-27},
+  // ...) need a row stride of 6 or 10 16-B units: CINP + 16 halves for CINP = 32 / 64
+  static constexpr int ROW = M16 ? CINP + 16 : CINP + 8;
   static_assert(KSTEPS % KS == 0, "k-steps must split evenly over the groups");
   // max over TW in {8, 16, 32} of (SH (TH - 1) + 3)(TW + 2)
   static constexpr int HALO_PIX = SH == 1 ? (PIX == 256 ? 340 : 204) : (PIX == 256 ? 594 : 330);
   static constexpr int HALO_F = HALO_PIX * ROW;                     // floats = hi + lo halves
   static constexpr int WRES_F = 9 * NP * ROW;                       // floats = hi + lo halves
-  static constexpr int EPI = NW * 1024 * KS;                        // epilogue slabs + partner sums
+  static constexpr int SLAB = epi_slab_floats<M16>();               // one 32x32 tile's slab
+  static constexpr int EPI = NW * SLAB * KS;                        // epilogue slabs + partner sums
   static constexpr int LDS = (HALO_F > EPI ? HALO_F : EPI) + WRES_F;
   static constexpr int PF = (HALO_PIX * QP + NT - 1) / NT;          // staged float4 per thread
 };
@@ -467,6 +480,14 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
   const int p_own = pw * 32 + li;
   const int abase = ((p_own / TW) * SH * HW + (p_own % TW)) * C::ROW + 8 * lh + 16 * C::KSG * kg;
   const int bbase = li * C::ROW + 8 * lh + 16 * C::KSG * kg;
+  // 16x16x32 form: pixel block q of the wave (pixels 16 q .. 16 q + 15), channel block q
+  int abase16[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int p = pw * 32 + 16 * q + (lane & 15);
+    abase16[q] = ((p / TW) * SH * HW + (p % TW)) * C::ROW + 8 * (lane >> 4) + 16 * C::KSG * kg;
+  }
+  const int bbase16 = (lane & 15) * C::ROW + 8 * (lane >> 4) + 16 * C::KSG * kg;
   // one tile; S = the register set this tile's successor-but-one is loaded into
   auto tile = [&](int t, auto setc) {
     constexpr int S = decltype(setc)::value;
@@ -480,25 +501,71 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
       pf_load(tn, setc);
     }
 #endif
-    f32x16 acc[1][1], accx;
+    f32x16 acc[1][1];
+    if constexpr (C::M16) {
+      // 16x16x32 form: a tap's KSG 16-deep steps are KSG / 2 32-deep ones; the wave's 32
+      // pixels x 32 channels are 2 x 2 blocks of 16 (lane l: pixel / channel l & 15 of a
+      // block, k 8 (l >> 4) .. +7), two accumulator sets as before (hi x hi; the cross terms)
+      f32x4 a4[2][2], x4[2][2];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { acc[0][0][r] = 0.f; accx[r] = 0.f; }
+      for (int pb = 0; pb < 2; ++pb)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          a4[pb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+          x4[pb][cb] = a4[pb][cb];
+        }
 #pragma unroll 3
-    for (int tap = 0; tap < (SPK_EXP == 3 ? 0 : 9); ++tap) {
-      const int aoff = abase + ((tap / 3) * HW + (tap % 3)) * C::ROW;
-      const int boff = tap * C::NP * C::ROW + bbase;
+      for (int tap = 0; tap < (SPK_EXP == 3 ? 0 : 9); ++tap) {
+        const int toff = ((tap / 3) * HW + (tap % 3)) * C::ROW;
 #pragma unroll
-      for (int s = 0; s < C::KSG; ++s) {
-        const f16x8 ah = *reinterpret_cast<const f16x8*>(hh + aoff + 16 * s);
-        const f16x8 al = *reinterpret_cast<const f16x8*>(hlo + aoff + 16 * s);
-        const f16x8 bh = *reinterpret_cast<const f16x8*>(wh + boff + 16 * s);
-        const f16x8 bl = *reinterpret_cast<const f16x8*>(wl + boff + 16 * s);
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[0][0], 0, 0, 0);
-        accx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, accx, 0, 0, 0);
-        accx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, accx, 0, 0, 0);
+        for (int s = 0; s < C::KSG / 2; ++s) {
+          f16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int ao = abase16[q] + toff + 32 * s;
+            ah[q] = *reinterpret_cast<const f16x8*>(hh + ao);
+            al[q] = *reinterpret_cast<const f16x8*>(hlo + ao);
+            const int bo = tap * C::NP * C::ROW + bbase16 + q * 16 * C::ROW + 32 * s;
+            bh[q] = *reinterpret_cast<const f16x8*>(wh + bo);
+            bl[q] = *reinterpret_cast<const f16x8*>(wl + bo);
+          }
+#pragma unroll
+          for (int pb = 0; pb < 2; ++pb)
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) {
+              a4[pb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[pb], bh[cb], a4[pb][cb], 0, 0, 0);
+              x4[pb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[pb], bl[cb], x4[pb][cb], 0, 0, 0);
+              x4[pb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[pb], bh[cb], x4[pb][cb], 0, 0, 0);
+            }
+        }
       }
+      // quadrant q = 2 pb + cb at elements 4q .. 4q + 3 (epilogue_tiles L16 layout)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          acc[0][0][4 * q + e] = a4[q >> 1][q & 1][e] * back + x4[q >> 1][q & 1][e] * back_x;
+    } else {
+      f32x16 accx;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { acc[0][0][r] = 0.f; accx[r] = 0.f; }
+#pragma unroll 3
+      for (int tap = 0; tap < (SPK_EXP == 3 ? 0 : 9); ++tap) {
+        const int aoff = abase + ((tap / 3) * HW + (tap % 3)) * C::ROW;
+        const int boff = tap * C::NP * C::ROW + bbase;
+#pragma unroll
+        for (int s = 0; s < C::KSG; ++s) {
+          const f16x8 ah = *reinterpret_cast<const f16x8*>(hh + aoff + 16 * s);
+          const f16x8 al = *reinterpret_cast<const f16x8*>(hlo + aoff + 16 * s);
+          const f16x8 bh = *reinterpret_cast<const f16x8*>(wh + boff + 16 * s);
+          const f16x8 bl = *reinterpret_cast<const f16x8*>(wl + boff + 16 * s);
+          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[0][0], 0, 0, 0);
+          accx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, accx, 0, 0, 0);
+          accx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, accx, 0, 0, 0);
+        }
+      }
+      acc[0][0] = acc[0][0] * back + accx * back_x;
     }
-    acc[0][0] = acc[0][0] * back + accx * back_x;
     __syncthreads();                                // halo reads done: the epilogue reuses it
     const int img = t / (ntx * nty), ty = (t / ntx) % nty, tx = t % ntx;
     const int y0 = ty * TH, x0 = tx * TW;
@@ -508,12 +575,18 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
       // 16 kg .. 16 kg + 15) -- bias, activation, two row-quad stores per lane -- so all
       // eight waves store (one group used to idle through the epilogue) and every wave issues
       // the same stores, which keeps the next halos' wait counts exact
-      float* slab = lds + (kg * C::NW + pw) * 1024;
+      constexpr int SROW = epi_srow<C::M16>();
+      float* slab = lds + (kg * C::NW + pw) * C::SLAB;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) slab[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[0][0][r];
+      for (int r = 0; r < 16; ++r) {
+        if constexpr (C::M16)
+          slab[(16 * (r >> 3) + 4 * (lane >> 4) + (r & 3)) * SROW + 16 * ((r >> 2) & 1) + (lane & 15)] = acc[0][0][r];
+        else
+          slab[((r & 3) + 8 * (r >> 2) + 4 * lh) * SROW + li] = acc[0][0][r];
+      }
       __syncthreads();
-      const float* s0 = lds + pw * 1024;
-      const float* s1 = lds + (C::NW + pw) * 1024;
+      const float* s0 = lds + pw * C::SLAB;
+      const float* s1 = lds + (C::NW + pw) * C::SLAB;
       const int c4 = (lane & 7) * 4, n = n0 + c4, M = d.nimg * H * W;
       float amax = 0.f;
       f32x4 o[2];
@@ -527,7 +600,7 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
           const int gy = y0 + p / TW, gx = x0 + p % TW;
           mq[q] = (gy < H && gx < W) ? (img * H + gy) * W + gx : -1;
           // group 0's partial + group 1's, then the bias: the order the two-step form used
-          o[q] = *reinterpret_cast<const f32x4*>(s0 + rl * 32 + c4) + *reinterpret_cast<const f32x4*>(s1 + rl * 32 + c4) +
+          o[q] = *reinterpret_cast<const f32x4*>(s0 + rl * SROW + c4) + *reinterpret_cast<const f32x4*>(s1 + rl * SROW + c4) +
                  bias4;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -553,7 +626,7 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
 #endif
     } else {
       if constexpr (KS > 1) {                       // group 1's partial sums -> group 0
-        float* part = lds + (C::NW + pw) * 1024;
+        float* part = lds + (C::NW + pw) * C::SLAB;
         if (kg == 1) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) part[r * 64 + lane] = acc[0][0][r];
@@ -566,7 +639,7 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
       }
       if (kg == 0) {
 #if SPK_EXP != 2
-        epilogue_tiles<1, 1, true, PLAIN>(d, lds, acc, pw, lane, n0, d.nimg * H * W, [&](int r) {
+        epilogue_tiles<1, 1, true, PLAIN, false, C::M16>(d, lds, acc, pw, lane, n0, d.nimg * H * W, [&](int r) {
           const int p = pw * 32 + r;
           const int gy = y0 + p / TW, gx = x0 + p % TW;
           return (gy < H && gx < W) ? (img * H + gy) * W + gx : -1;
