@@ -473,13 +473,13 @@ bool use_x3() {
   return x3;
 }
 
-// x3 tile override for experiments: SPK_X3_TILE=128x128 | 256x128 | 128x256
+// x3 tile override for experiments: SPK_X3_TILE=128x128 | 256x128 | 128x256 | 64x128
 int x3_tile() {
   static const int t = [] {
     const char* e = std::getenv("SPK_X3_TILE");
     if (!e) return 0;
     const std::string v(e);
-    return v == "256x128" ? 1 : v == "128x256" ? 2 : v == "128x128" ? 3 : 0;
+    return v == "256x128" ? 1 : v == "128x256" ? 2 : v == "128x128" ? 3 : v == "64x128" ? 4 : 0;
   }();
   return t;
 }
@@ -500,11 +500,18 @@ Cfg select_cfg(const ConvDesc& d) {
   if (d.N <= 32) return (M + 255) / 256 >= 512 ? Cfg{256, 32, bk, 8, 1} : Cfg{64, 32, bk, 2, 1};
   if (d.N <= 64) return {256, 64, bk, 4, 2};
   if (M <= 4096) return {64, 128, bk, 1, 4};
+  // pre-activation GEMMs with fewer 128x128 blocks than CUs (CAM++'s dense-layer linear1,
+  // M = 25,344 pixels: 198 blocks) take 64-row tiles: every CU busy and twice the loads in
+  // flight (measured 2.86 -> 1.88 ms over CAM++'s 52 dense layers; CAM++'s xvector.tdnn, 198
+  // blocks without a pre-activation, and ECAPA's 396-block GEMMs measured slower with it:
+  // profiles/r06_ablation/campplus_pre_tile_ab.txt)
+  if (d.s0.pre_scale && ((M + 127) / 128) * ((d.N + 127) / 128) < device_cus()) return {64, 128, bk, 1, 4};
   if (use_x3() && d.wh && !d.wbig) {
     const int t = x3_tile();
     if (t == 1) return {256, 128, 32, 4, 2};
     if (t == 2) return {128, 256, 32, 2, 4};
     if (t == 3) return {128, 128, 32, 2, 4};
+    if (t == 4) return {64, 128, 32, 1, 4};
     // measured per layer (tools/tile_exp.sh, round 3): with one accumulator the 128x128 tile
     // keeps two blocks (four waves per SIMD) per CU and is the fastest or within 2 % on every
     // x3 GEMM of ERes2NetV2 / ERes2Net-large (all-128x128 27.0 ms vs 28.6 for round 2's
