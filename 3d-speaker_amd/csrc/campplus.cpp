@@ -229,7 +229,8 @@ void build_campplus(Builder& b, int T) {
         throw SpkError(SPK_E_UNSUPPORTED, q + ": channel counts must be multiples of 4");
       const Packed* pre = &m.pack_post_affine(q + ".pre", q + ".nonlinear1.batchnorm", ChanMap::dense(cin));
       const Packed& l1 = m.pack(q + ".linear1", ChanMap::dense(bnc),
-                                {Part{q + ".linear1.weight", "", q + ".nonlinear2.batchnorm", ChanMap::dense(cin), 0, 0}}, cin);
+                                {Part{q + ".linear1.weight", "", q + ".nonlinear2.batchnorm", ChanMap::dense(cin), 0, 0}}, cin,
+                                pre->pre_bits);
       const std::string c = q + ".cam_layer";
       const Packed& cl1 = m.pack(c + ".linear1", ChanMap::dense(red),
                                  {Part{c + ".linear1.weight", c + ".linear1.bias", "", ChanMap::dense(bnc), 0, 0}}, bnc);
@@ -289,7 +290,7 @@ void build_campplus(Builder& b, int T) {
     const Packed& tp = m.pack(t, ChanMap::dense(cout),
                               {Part{t + ".linear.weight", "", last ? "xvector.out_nonlinear.batchnorm" : "",
                                     ChanMap::dense(bk.c_fin), 0, 0}},
-                              bk.c_fin);
+                              bk.c_fin, pre->pre_bits);
     b.macs_per_utt += T2d * cout * bk.c_fin;
     Buf dst;
     int ldd;

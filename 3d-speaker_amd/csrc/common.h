@@ -80,10 +80,6 @@ struct ConvDesc {
   // null: that kernel is not used)
   const uint16_t* wf = nullptr;
   const int* range_in = nullptr;  // scaled split (below): the forward's range word, read for the operand scale
-  // extra operand scale bits for a GEMM whose loader amplifies its operand (CAM++'s BN-ReLU
-  // pre-activation, s0.pre_scale): relu(psc x + psh) can exceed the 2x growth bound the word
-  // assumes, so the operand is scaled by a further 2^-range_bits (Builder::conv, pre_range_bits)
-  int range_bits = 0;
 };
 
 // fp16x3 range guard.  The split-precision GEMMs represent an operand as two fp16 values,
@@ -110,9 +106,12 @@ struct ConvDesc {
 //    |psc| |x| + |psh|) breaks the 2x growth bound by up to P = max_c max(|psc|, |psh| / 2^14):
 //    with |x| < 2^(e+2) (e: the word's exponent, 13 when clear) the operand is below
 //    1.5 P 2^(e+2), so a further 2^-b with P <= 1.3 * 2^b keeps the scaled operand below
-//    1.95 * 2^15 < 65504 (host: pre_range_bits, ConvDesc::range_bits; applied in the twin
-//    plans too).  A block may read a larger word than another (producers of its own launch
-//    raising it meanwhile): each block undoes its own scale, so every output is consistent.
+//    1.95 * 2^15 < 65504.  That 2^-b is folded into the affine on the host (psc 2^-b,
+//    psh 2^-b: relu is positively homogeneous and power-of-two scaling is exact) and 2^b into
+//    the GEMM's packed weights (Model::pack wexp; the products are unchanged, bit for bit), so
+//    no kernel sees it: the GEMM keeps its in-range instance while the word is clear, and the
+//    exact-fp32 kernels and the twin plans read the same packed operands.  A block may read a larger word than another (producers of its own
+//    launch raising it meanwhile): each block undoes its own scale, so every output is consistent.
 constexpr float kRangeLimit = 16384.0f;
 // the tiled fp16x3 GEMM scales the weights' hi plane by 2^11 (conv_gemm.hip): 31.5 * 2^11 < 65504
 constexpr float kX3WeightLimit = 31.5f;
@@ -121,15 +120,25 @@ __device__ __forceinline__ void range_note(int* flag, float amax) {
   if (flag && amax >= kRangeLimit) atomicMax(flag, __float_as_int(amax));
 }
 // operand scale of a scaled-split GEMM (above): 1 while the word is clear (or absent, or
-// non-finite: the result is inf / NaN either way), else 2^-s with word * 2^-s in [2^13, 2^14);
-// times 2^-bits for an amplifying operand loader (ConvDesc::range_bits)
-__device__ __forceinline__ float range_scale(const int* word, int bits = 0) {
+// non-finite: the result is inf / NaN either way), else 2^-s with word * 2^-s in [2^13, 2^14)
+__device__ __forceinline__ float range_scale(const int* word) {
+  if (!word) return 1.f;
+  const int w = *word;
+  if (w < 0x46800000 || w >= 0x7F800000) return 1.f;       // below 2^14 (i.e. 0), or inf / NaN
+  const int e = (w >> 23) - 127;                             // word in [2^e, 2^(e+1)), e >= 14
+  return __int_as_float((127 - (e - 13)) << 23);             // 2^-(e-13)
+}
+// the same value without early returns: the LDS-DMA, pointwise and halo kernels measured
+// 2 % faster with this form on ECAPA (its 256x256 GEMMs), while the tiled GEMM's 128-VGPR
+// allocation spills inside its in-range instance with it (PRE instance 42 -> 58 spilled VGPRs,
+// CAM++ dense layers +70 %): each keeps the form it was tuned with
+__device__ __forceinline__ float range_scale_flat(const int* word) {
   int s = 0;
   if (word) {
     const int w = *word;
     if (w >= 0x46800000 && w < 0x7F800000) s = ((w >> 23) - 127) - 13;   // word in [2^e, 2^(e+1)), e >= 14
   }
-  return __int_as_float((127 - min(s + bits, 126)) << 23);   // 2^-(s + bits), kept normal
+  return __int_as_float((127 - min(s, 126)) << 23);   // 2^-s, kept normal
 }
 // 2^k * sc and 2^k / sc of a power-of-two scale by exponent arithmetic (scalar integer ops:
 // the values stay in SGPRs instead of taking a VGPR each for a float multiply / divide)

@@ -356,7 +356,7 @@ conv3x3_halo_x3_kernel(const ConvDesc d, int nsplit) {
   SPK_GATE(d.run_if);
   using C = HaloX3Cfg<CIN, PIX, KS, SH>;
   // scaled split (common.h): operand x 2^-s at staging, accumulators x 2^s after the taps
-  const float sc = range_scale(d.range_in, d.range_bits), back = pow2_div(sc, 0), back_x = pow2_div(sc, -11);
+  const float sc = range_scale_flat(d.range_in), back = pow2_div(sc, 0), back_x = pow2_div(sc, -11);
   typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
   typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) float lds[C::LDS];

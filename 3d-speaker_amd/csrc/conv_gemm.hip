@@ -414,7 +414,7 @@ template <int BM, int BN, int WM, int WN, bool S1, bool ADD, bool PRE, bool BUF,
 __device__ __forceinline__ void conv_gemm_f16_entry(const ConvDesc& d) {
   SPK_GATE(d.run_if);
   __shared__ __attribute__((aligned(16))) float lds[X3Cfg<BM, BN, WM, WN, X1>::LDS_FLOATS];
-  const float sc = range_scale(d.range_in, d.range_bits);
+  const float sc = range_scale(d.range_in);
   if (sc == 1.0f) conv_gemm_f16_body<BM, BN, WM, WN, S1, ADD, PRE, BUF, X1, false>(d, lds, 1.0f);
   else conv_gemm_f16_body<BM, BN, WM, WN, S1, ADD, PRE, BUF, X1, true>(d, lds, sc);
 }
@@ -500,12 +500,6 @@ Cfg select_cfg(const ConvDesc& d) {
   if (d.N <= 32) return (M + 255) / 256 >= 512 ? Cfg{256, 32, bk, 8, 1} : Cfg{64, 32, bk, 2, 1};
   if (d.N <= 64) return {256, 64, bk, 4, 2};
   if (M <= 4096) return {64, 128, bk, 1, 4};
-  // pre-activation GEMMs with fewer 128x128 blocks than CUs (CAM++'s dense-layer linear1,
-  // M = 25,344 pixels: 198 blocks) take 64-row tiles: every CU busy and twice the loads in
-  // flight (measured 2.86 -> 1.88 ms over CAM++'s 52 dense layers; CAM++'s xvector.tdnn, 198
-  // blocks without a pre-activation, and ECAPA's 396-block GEMMs measured slower with it:
-  // profiles/r06_ablation/campplus_pre_tile_ab.txt)
-  if (d.s0.pre_scale && ((M + 127) / 128) * ((d.N + 127) / 128) < device_cus()) return {64, 128, bk, 1, 4};
   if (use_x3() && d.wh && !d.wbig) {
     const int t = x3_tile();
     if (t == 1) return {256, 128, 32, 4, 2};

@@ -133,7 +133,7 @@ template <int BM, int BN, int WM, int WN, int OP2>
 __global__ void __launch_bounds__(64 * WM * WN, (FCfg<BM, BN, WM, WN>::WAVES_PER_EU))
 conv_gemm_x3f_kernel(const ConvDesc d) {
   SPK_GATE(d.run_if);
-  const float sc = range_scale(d.range_in, d.range_bits);            // scaled split: operand x 2^-s (common.h)
+  const float sc = range_scale_flat(d.range_in);            // scaled split: operand x 2^-s (common.h)
   using C = FCfg<BM, BN, WM, WN>;
   constexpr bool ADD = OP2 == 1, S1 = OP2 == 2;
   constexpr int TM = C::TM, TN = C::TN, ROWS = C::ROWS, NT = C::NT;

@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(512, 1)
 pw_gemm_x3_kernel(const ConvDesc d) {
   SPK_GATE(d.run_if);
   // scaled split (common.h): operand x 2^-s at staging, accumulators x 2^s in the epilogue
-  const float sc = range_scale(d.range_in, d.range_bits), back = pow2_div(sc, 0), back_x = pow2_div(sc, -11);
+  const float sc = range_scale_flat(d.range_in), back = pow2_div(sc, 0), back_x = pow2_div(sc, -11);
   using C = PwCfg<KP, BN>;
   __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
   _Float16* Bh = reinterpret_cast<_Float16*>(lds);

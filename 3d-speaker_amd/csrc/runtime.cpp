@@ -81,9 +81,12 @@ void Model::bn_fold(const std::string& bn, int n, std::vector<double>& s, std::v
   }
 }
 
-const Packed& Model::pack(const std::string& name, const ChanMap& out, const std::vector<Part>& parts, int K) {
+const Packed& Model::pack(const std::string& name, const ChanMap& out, const std::vector<Part>& parts, int K, int wexp) {
   auto it = packed.find(name);
-  if (it != packed.end()) return it->second;
+  if (it != packed.end()) {
+    if (it->second.wexp != wexp) throw SpkError(SPK_E_INVALID, "internal: " + name + " packed with two weight scales");
+    return it->second;
+  }
   if (uploaded) throw SpkError(SPK_E_INVALID, "internal: pack after upload: " + name);
   const int N = out.n_phys;
   const int Kp = round_up(K, 32);
@@ -147,6 +150,9 @@ const Packed& Model::pack(const std::string& name, const ChanMap& out, const std
     }
     p.kcb = 1;
   }
+  if (wexp)
+    for (double& v : wd) v = std::ldexp(v, wexp);   // before the fp32 rounding: the same as scaling after it
+  p.wexp = wexp;
   std::vector<float> wf(wd.begin(), wd.end()), bf(bd.begin(), bd.end());
   for (float v : wf) p.wmax = std::max(p.wmax, std::fabs(v));
   for (int n = 0; n < N; ++n) {
@@ -178,6 +184,16 @@ const Packed& Model::pack_post_affine(const std::string& name, const std::string
   }
   p.ps_off = put(ps);
   p.pt_off = put(pt);
+  p.pre_bits = pre_range_bits(p);
+  if (p.pre_bits) {   // powers of two: exact (the fp32 values stay normal for any sane affine)
+    std::vector<float> ps2(ps), pt2(pt);
+    for (int c = 0; c < out.n_phys; ++c) {
+      ps2[c] = std::ldexp(ps[c], -p.pre_bits);
+      pt2[c] = std::ldexp(pt[c], -p.pre_bits);
+    }
+    p.ps2_off = put(ps2);
+    p.pt2_off = put(pt2);
+  }
   return packed.emplace(key, p).first->second;
 }
 
@@ -250,9 +266,13 @@ int pre_range_bits(const Packed& pre) {
 void Builder::conv(const std::string& name, ConvDesc d, const Packed& p, const ConvIO& io, bool use_bias) {
   if (!plan) return;
   if (io.pre) {
-    d.s0.pre_scale = m.dptr(io.pre->ps_off);
-    d.s0.pre_shift = m.dptr(io.pre->pt_off);
-    d.range_bits = pre_range_bits(*io.pre);
+    // the affine times 2^-b, the weights times 2^b (common.h range guard): every kernel that
+    // takes a pre-activation (tiled fp16x3 / fp16 / exact fp32) computes the same products
+    const bool s2 = io.pre->pre_bits > 0;
+    if (p.wexp != io.pre->pre_bits)
+      throw SpkError(SPK_E_INVALID, "internal: " + name + " weights not packed for its pre-activation scale");
+    d.s0.pre_scale = m.dptr(s2 ? io.pre->ps2_off : io.pre->ps_off);
+    d.s0.pre_shift = m.dptr(s2 ? io.pre->pt2_off : io.pre->pt_off);
   } else if (d.s0.pre_scale) {
     // the operand bound of the scaled split needs the pre-activation's host-side extremes
     throw SpkError(SPK_E_INVALID, "internal: pre-activation without its packed affine: " + name);

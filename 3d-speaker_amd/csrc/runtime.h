@@ -105,6 +105,12 @@ struct Packed {
   size_t w_off = 0, b_off = 0;
   int N = 0, K = 0, Kp = 0;
   size_t ps_off = SIZE_MAX, pt_off = SIZE_MAX;   // optional post-activation affine
+  // the same affine times 2^-pre_bits, for a GEMM's pre-activation loader (common.h range
+  // guard, pre_range_bits; SIZE_MAX while pre_bits = 0); that GEMM's weights are packed times
+  // 2^pre_bits (wexp)
+  size_t ps2_off = SIZE_MAX, pt2_off = SIZE_MAX;
+  int pre_bits = 0;
+  int wexp = 0;                                   // weights packed times 2^wexp (Model::pack)
   bool has_bias = false;
   float wmax = 0.f;                               // max |w| of the packed matrix
   double l1max = 0.0;                             // max over output channels of sum_k |w| (bounds)
@@ -163,7 +169,9 @@ struct Model {
   const uint16_t* dlo(size_t off) const { return dsplit ? dsplit + dweights_bytes / sizeof(float) + off : nullptr; }
   // fold BN (+conv bias) into per-output-channel (scale, shift) in double precision
   void bn_fold(const std::string& bn, int n, std::vector<double>& s, std::vector<double>& t, double eps = 1e-5) const;
-  const Packed& pack(const std::string& name, const ChanMap& out, const std::vector<Part>& parts, int K);
+  // wexp: weights (not bias) times 2^wexp, for a GEMM behind a pre-activation packed times
+  // 2^-wexp (Packed::pre_bits; exact: the products are unchanged)
+  const Packed& pack(const std::string& name, const ChanMap& out, const std::vector<Part>& parts, int K, int wexp = 0);
   const Packed& pack_post_affine(const std::string& name, const std::string& bn, const ChanMap& out);
 };
 
@@ -224,7 +232,8 @@ struct Builder {
 };
 
 // operand scale bits for a GEMM whose loader applies the pre-activation `pre` (common.h
-// ConvDesc::range_bits): the smallest b >= 0 with max_c max(|psc|, |psh| / 2^14) <= 1.3 * 2^b
+// range guard; Packed::pre_bits / wexp): the smallest b >= 0 with
+// max_c max(|psc|, |psh| / 2^14) <= 1.3 * 2^b
 int pre_range_bits(const Packed& pre);
 
 void build_eres2net(Builder& b, int T, bool v2);

@@ -5,7 +5,8 @@ layers.py:113-149; the transits' `nonlinear`, layers.py:183-196) inside the GEMM
 loader, after the producer of x noted its largest output in the range word.  relu(psc x + psh)
 can exceed the 2x growth bound the word assumes, by up to P = max_c max(|psc|, |psh| / 2^14), so
 those GEMMs scale their operand by a further 2^-b with P <= 1.3 * 2^b (common.h,
-runtime.cpp pre_range_bits).  The construction below (TDNN output BN scaled, block1.tdnnd1's
+runtime.cpp pre_range_bits): the affine is packed times 2^-b and the GEMM's weights times 2^b
+(the products unchanged), so no kernel sees the bits.  The construction below (TDNN output BN scaled, block1.tdnnd1's
 nonlinear1 running_var shrunk to 1e-2, so psc ~ 12) drives the scaled operand past fp16's
 65504 under the word-only scale, both with the word clear (activations just below 2^14) and
 set; the CPU test pins that arithmetic, the GPU test the forward against fp64."""
