@@ -24,7 +24,7 @@
 #include "conv_loader.h"
 
 #ifndef SPK_GEXP
-#define SPK_GEXP 0   // ablation builds only (tools/gemm_exp.sh): 1 no MFMA, 2 no split, 3 no
+#define SPK_GEXP 0   // ablation builds only (tools/gemm_exp.sh): 6 no epilogue, 1 no MFMA, 2 no split, 3 no
                      // in-loop loads, 5 no in-loop LDS stores; 0 = the product kernel
 #endif
 
@@ -395,7 +395,20 @@ __device__ __forceinline__ void conv_gemm_f16_body(const ConvDesc& d, float* lds
       for (int j = 0; j < TN; ++j)
         acc[i][j] *= back;
   }
+#if SPK_GEXP == 6
+  {   // ablation: no epilogue (every accumulator kept live through one conditional store)
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sum += acc[i][j][r];
+    if (sum == 1234.5f) d.out[tid] = sum;
+  }
+#else
   epilogue_tiles<TM, TN>(d, lds, acc, wave, lane, n0 + wn * C::WTN, M, [&](int r) { return m0 + wm * C::WTM + r; });
+#endif
 }
 
 // A 128-VGPR budget (4 waves per SIMD) for the <= 128x128 tiles: the in-range instance fits
