@@ -100,3 +100,19 @@ def test_hot_preactivation_matches_fp64(factor):
     assert np.isfinite(out).all()
     err = helpers.rel_err(out, ref).max()
     assert err < tol, (err, tol)
+
+
+def test_emulated_forward_with_folded_pre_bits():
+    """The host emulation (tests/emu) runs the real plan builder and packing: the 2^-b folded
+    into block1's packed BN-ReLU affine and the 2^b folded into its weights must cancel, so the
+    emulated forward (exact GEMMs) reproduces fp64 like the unmodified model does."""
+    from emu_runner import EmuModel
+    m, sd = _hot_state(3e3)
+    feats = torch.from_numpy(helpers.golden('campplus')['feats2'][:1])
+    ref = R.forward('campplus', sd, feats.double()).numpy()
+    ref32 = R.forward('campplus', {k: v.float() if v.is_floating_point() else v for k, v in sd.items()},
+                      feats).numpy()
+    tol = max(1e-4, 1.5 * helpers.rel_err(ref32, ref).max())
+    out = EmuModel(m)(feats).numpy()
+    assert np.isfinite(out).all()
+    assert helpers.rel_err(out, ref).max() < tol
